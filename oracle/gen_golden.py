@@ -1,0 +1,223 @@
+"""ORACLE (test infrastructure only): generate ``tests/golden/*.npz``.
+
+Run in the build container only (``/root/reference`` does not exist on the GPU box):
+
+    python -m oracle.gen_golden
+
+What it does, per fixture:
+
+1. Regenerate seeded weights/images (``synth.make_weights`` / ``make_images``).
+2. Run the **reference's own** glue — ``src/model_swin.py`` + ``src/inference.py``
+   (batched greedy) and ``app/src/model_swin.py`` + ``app/src/im2latex.py``
+   (serving) — imported unmodified from ``/root/reference``.  torchvision is not
+   installed, so a stand-in package whose ``models.swin_t`` returns the restated
+   module (``oracle/swin_ref.py``, pinned separately against HF Swin) is put on
+   ``sys.path``; everything else (stem replacement, projection, decoder,
+   ``nn.TransformerDecoder``, greedy loop, detokeniser, confidence) is the
+   reference's code.
+3. Run the oracle restatement (``oracle/model_ref.py``) on the same inputs and
+   assert it reproduces the reference glue bit-for-bit (token ids, logits).
+4. Save inputs' seeds, token ids, first-step logits, per-step top-2 margins,
+   encoder memory and per-stage checksums as small ``.npz`` fixtures.
+
+Weights and images are *not* stored: the tests regenerate them from the seeds.
+"""
+from __future__ import annotations
+
+import importlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import textwrap
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+STUB_INIT = "from . import models  # noqa\n"
+STUB_MODELS = textwrap.dedent(f"""
+    import sys
+    sys.path.insert(0, {REPO!r})
+    from oracle.swin_ref import swin_t  # noqa: F401  (restated torchvision swin_t)
+
+    class Swin_T_Weights:
+        DEFAULT = None
+
+    class ResNet18_Weights:
+        DEFAULT = None
+
+    def resnet18(*a, **k):
+        raise RuntimeError("resnet18 is not part of this fixture")
+""")
+
+
+def _pkg():
+    sys.path.insert(0, REPO)
+    return importlib.import_module("handwritten-math-ocr-api_amd")
+
+
+def _stub_dir():
+    d = tempfile.mkdtemp(prefix="mocr_tv_")
+    os.makedirs(os.path.join(d, "torchvision", "models"))
+    with open(os.path.join(d, "torchvision", "__init__.py"), "w") as f:
+        f.write(STUB_INIT)
+    with open(os.path.join(d, "torchvision", "models", "__init__.py"), "w") as f:
+        f.write(STUB_MODELS)
+    return d
+
+
+def apply_eos_boost(weights, boost):
+    if boost:
+        weights["decoder.fc_out.bias"] = weights["decoder.fc_out.bias"].copy()
+        weights["decoder.fc_out.bias"][2] += np.float32(boost)
+    return weights
+
+
+# ---------------------------------------------------------------------------------------------
+# Child process: reference glue (one process per reference tree, module names collide).
+# ---------------------------------------------------------------------------------------------
+CHILD = r"""
+import sys, os, json, importlib
+import numpy as np, torch
+spec = json.loads(sys.argv[1])
+sys.path.insert(0, spec["stub"]); sys.path.insert(0, spec["src"]); sys.path.insert(0, spec["repo"])
+os.makedirs(spec["cwd"], exist_ok=True); os.chdir(spec["cwd"])
+pkg = importlib.import_module("handwritten-math-ocr-api_amd")
+from oracle.gen_golden import apply_eos_boost
+w = apply_eos_boost(pkg.synth.make_weights(spec["seed"], spec["variant"]), spec["eos_boost"])
+imgs = torch.from_numpy(pkg.synth.make_images(spec["B"], spec["H"], spec["W"], spec["img_seed"], spec["img_kind"]))
+vocab, idx2char = pkg.synth.synthetic_vocab(w["decoder.fc_out.weight"].shape[0])
+import config as cfgmod
+import model_swin
+torch.manual_seed(0)
+model = model_swin.FormulaRecognitionModel(len(vocab))
+sd = {k: torch.from_numpy(v) for k, v in w.items()}
+missing, unexpected = model.load_state_dict(sd, strict=False)
+assert not unexpected, unexpected
+assert all(k.startswith("encoder.swin.") or k.endswith("relative_position_index") or k == "decoder.tgt_mask"
+           for k in missing), missing
+model.eval()
+out = {}
+if spec["mode"] == "batch":
+    cfgmod.config.max_seq_len = spec["steps"]          # loop count only; pos table already has 150 rows
+    import inference
+    rec = []
+    orig = model.decoder.forward
+    def hooked(enc, tgt):
+        o = orig(enc, tgt); rec.append(o[:, -1, :].clone()); return o
+    model.decoder.forward = hooked
+    strings = inference.predict(imgs, model, vocab, idx2char, "cpu")
+    logits = torch.stack(rec, 1)                       # [B, n, V]
+    out["strings"] = strings
+    out["ids"] = logits.argmax(-1).tolist()
+    np.save(spec["logits_path"], logits.numpy())
+else:
+    import im2latex
+    formula, conf = im2latex.predict(model, imgs[:1], vocab, idx2char, "cpu")
+    out["formula"] = formula; out["confidence"] = conf
+print("JSON" + json.dumps(out))
+"""
+
+
+def run_reference(mode, *, seed, variant, eos_boost, B, H, W, img_seed, img_kind, steps, stub):
+    src = os.path.join(REF, "src" if mode == "batch" else "app/src")
+    with tempfile.TemporaryDirectory(prefix="mocr_ref_") as td:
+        spec = dict(mode=mode, seed=seed, variant=variant, eos_boost=eos_boost, B=B, H=H, W=W,
+                    img_seed=img_seed, img_kind=img_kind, steps=steps, stub=stub, src=src, repo=REPO,
+                    cwd=os.path.join(td, "run"), logits_path=os.path.join(td, "logits.npy"))
+        r = subprocess.run([sys.executable, "-c", CHILD, json.dumps(spec)], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"reference run failed:\n{r.stdout}\n{r.stderr}")
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("JSON")][-1]
+        out = json.loads(line[4:])
+        if mode == "batch":
+            out["logits"] = np.load(spec["logits_path"])
+        return out
+
+
+def make_batch_fixture(name, *, seed, variant, eos_boost, B, H, W, img_seed=1000, img_kind="uniform",
+                       steps, stop, n_logit_steps, stub, n_mem=2):
+    pkg = _pkg()
+    from oracle import model_ref
+    w = apply_eos_boost(pkg.synth.make_weights(seed, variant), eos_boost)
+    imgs = pkg.synth.make_images(B, H, W, img_seed, img_kind)
+    vocab, idx2char = pkg.synth.synthetic_vocab(w["decoder.fc_out.weight"].shape[0])
+    model = model_ref.build_model(w)
+    mem, stages = model_ref.encode(model, torch.from_numpy(imgs), stages=True)
+    ys, logits = model_ref.greedy_decode(model, memory=mem, max_steps=steps, stop=stop, record_logits=True)
+    logits = torch.stack(logits, 1).numpy()
+    strings = [model_ref.detokenize(s, idx2char) for s in ys]
+
+    glue = None
+    if stop == "batch":
+        glue = run_reference("batch", seed=seed, variant=variant, eos_boost=eos_boost, B=B, H=H, W=W,
+                             img_seed=img_seed, img_kind=img_kind, steps=steps, stub=stub)
+        ref_ids = np.asarray(glue["ids"])
+        assert np.array_equal(ref_ids, ys[:, 1:].numpy()), f"{name}: oracle ids differ from reference glue"
+        assert np.array_equal(glue["logits"], logits), f"{name}: oracle logits differ from reference glue"
+        assert glue["strings"] == strings, f"{name}: detokenised strings differ"
+    top2 = np.sort(logits, -1)[..., -2:]
+    margins = (top2[..., 1] - top2[..., 0]).astype(np.float32)
+    np.savez_compressed(
+        os.path.join(GOLDEN, name + ".npz"),
+        meta=json.dumps(dict(seed=seed, variant=variant, eos_boost=eos_boost, B=B, H=H, W=W, img_seed=img_seed,
+                             img_kind=img_kind, steps=steps, stop=stop, glue_checked=glue is not None,
+                             strings=strings)),
+        ids=ys.numpy().astype(np.int32),
+        logits=logits[:n_mem, :n_logit_steps].astype(np.float32),
+        margins=margins,
+        memory=mem[:n_mem].numpy().astype(np.float32),
+        stage_sum=np.array([[float(s[i].double().sum()) for s in stages] for i in range(B)]),
+        stage_abs=np.array([[float(s[i].double().abs().sum()) for s in stages] for i in range(B)]),
+    )
+    print(f"{name}: ids {tuple(ys.shape)} min-margin {margins.min():.2e} glue={'ok' if glue else '-'}")
+
+
+def make_serving_fixture(name, *, seed, variant, eos_boost, H, W, img_seed, img_kind, stub):
+    pkg = _pkg()
+    from oracle import model_ref
+    w = apply_eos_boost(pkg.synth.make_weights(seed, variant), eos_boost)
+    img = pkg.synth.make_images(1, H, W, img_seed, img_kind)
+    model = model_ref.build_model(w)
+    toks, lp_sum, conf = model_ref.serving_predict(model, torch.from_numpy(img))
+    ref = run_reference("serve", seed=seed, variant=variant, eos_boost=eos_boost, B=1, H=H, W=W,
+                        img_seed=img_seed, img_kind=img_kind, steps=150, stub=stub)
+    assert abs(ref["confidence"] - conf) <= 1e-7 * max(1.0, abs(conf)), (ref["confidence"], conf)
+    np.savez_compressed(
+        os.path.join(GOLDEN, name + ".npz"),
+        meta=json.dumps(dict(seed=seed, variant=variant, eos_boost=eos_boost, H=H, W=W, img_seed=img_seed,
+                             img_kind=img_kind, formula=ref["formula"], confidence=ref["confidence"],
+                             log_probs_sum=lp_sum, glue_checked=True)),
+        tokens=np.asarray(toks, dtype=np.int32),
+    )
+    print(f"{name}: {len(toks)} tokens conf={ref['confidence']:.6g} formula[:60]={ref['formula'][:60]!r}")
+
+
+def main():
+    torch.set_num_threads(max(1, len(os.sched_getaffinity(0))))
+    os.makedirs(GOLDEN, exist_ok=True)
+    stub = _stub_dir()
+    # 384x384, perturbed weights, 128 fixed steps (BASELINE config shape; ids checked via glue with EOS unreachable).
+    make_batch_fixture("g384_b2_pert", seed=11, variant="perturbed", eos_boost=0.0, B=2, H=384, W=384,
+                       steps=128, stop="batch", n_logit_steps=8, stub=stub)
+    # 384x384 with the reference-init distributions (what bench.py runs).
+    make_batch_fixture("g384_b1_init", seed=1234, variant="init", eos_boost=0.0, B=1, H=384, W=384,
+                       steps=32, stop="batch", n_logit_steps=4, stub=stub)
+    # 96x320 serving shape: padded maps, shift disabled on one axis in stages 3-4; EOS reachable so the
+    # batch-global stop and post-EOS generation are exercised.
+    make_batch_fixture("g96x320_b4_eos", seed=21, variant="perturbed", eos_boost=1.72, B=4, H=96, W=320,
+                       img_kind="ink", steps=150, stop="batch", n_logit_steps=4, stub=stub, n_mem=4)
+    # serving im2latex.predict (batch 1, confidence, tokens_to_latex + clean_latex_output)
+    make_serving_fixture("serve96x320_eos", seed=21, variant="perturbed", eos_boost=1.72, H=96, W=320,
+                         img_seed=1001, img_kind="ink", stub=stub)
+    make_serving_fixture("serve96x320_empty", seed=21, variant="perturbed", eos_boost=60.0, H=96, W=320,
+                         img_seed=1002, img_kind="ink", stub=stub)
+
+
+if __name__ == "__main__":
+    main()
