@@ -1,2 +1,8 @@
-"""MI355X-native engine for the Swin-T + 8-layer decoder greedy-decode hot path."""
-from . import synth  # noqa: F401
+"""MI355X-native engine for the Swin-T + 8-layer decoder greedy-decode hot path of
+PTD504/handwritten-math-ocr-api.
+
+The package directory name contains hyphens, so import it with
+``importlib.import_module("handwritten-math-ocr-api_amd")``.
+"""
+from . import synth, weights  # noqa: F401
+from .engine import DecodeResult, Engine, MocrError, load_library  # noqa: F401

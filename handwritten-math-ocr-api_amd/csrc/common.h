@@ -1,0 +1,78 @@
+// Shared device/host helpers for the gfx950 engine.  Wave = 64 lanes everywhere.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cmath>
+
+namespace mocr {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int kWave = 64;
+constexpr int kWin = 7;        // Swin window
+constexpr int kWinTok = 49;    // tokens per window
+constexpr int kHeadDim = 32;   // Swin and decoder head dim (96/3 ... 768/24; 256/8)
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Exact (erf) GELU, torch.nn.GELU() default: x * 0.5 * (1 + erf(x / sqrt(2))).
+__device__ __forceinline__ float gelu_erf(float x) {
+  return x * 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
+}
+
+// Region id along one axis of torchvision's shifted-window attention mask, built on
+// the padded map of size P with window 7 and shift s.  Mirrors the nine slice
+// assignments h_slices = ((0,-7), (-7,-s), (-s,None)) including the python-slice
+// behaviour for s == 0 ((-0, None) is the whole axis, so the last slice wins).
+__device__ __forceinline__ int shift_region(int y, int P, int s) {
+  if (s == 0) return 2;
+  return (y >= P - kWin) + (y >= P - s);
+}
+
+// Step/stop state of a greedy decode, read by every decode kernel (device memory,
+// so one captured graph serves every step).
+struct DecodeState {
+  int t;          // index of the step being run (position of the fed token)
+  int done;       // 1 once the decode must stop (all rows finished or max_steps reached)
+  int nfinished;  // rows that have produced EOS
+  int nsteps;     // steps run when done
+  int max_steps;
+  int stop_mode;  // 0 = batch-global stop, 1 = none
+  int pad[2];
+};
+
+}  // namespace mocr
+
+#define MOCR_HIP_CHECK(expr)                                                   \
+  do {                                                                         \
+    hipError_t _e = (expr);                                                    \
+    if (_e != hipSuccess) {                                                    \
+      throw mocr::HipError(_e, #expr, __FILE__, __LINE__);                     \
+    }                                                                          \
+  } while (0)
+
+#include <stdexcept>
+#include <string>
+
+namespace mocr {
+struct HipError : std::runtime_error {
+  hipError_t code;
+  HipError(hipError_t e, const char* expr, const char* file, int line)
+      : std::runtime_error(std::string(hipGetErrorString(e)) + " at " + file + ":" +
+                           std::to_string(line) + " (" + expr + ")"),
+        code(e) {}
+};
+}  // namespace mocr

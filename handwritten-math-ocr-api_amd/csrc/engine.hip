@@ -1,0 +1,775 @@
+// libmathocr.so: engine state, weight layout, encoder schedule, hipGraph-captured
+// decode loop, and the C-ABI of include/mathocr.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/mathocr.h"
+#include "kernels.h"
+
+using namespace mocr;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+constexpr int kStages = 4;
+constexpr int kDepth[kStages] = {2, 2, 6, 2};
+constexpr int kHeads[kStages] = {3, 6, 12, 24};
+constexpr int kEmbed = 96;
+constexpr int kEncDim = 768;
+constexpr int kDecodeChunk = 8;  // steps per captured graph
+
+struct StageGeom {
+  int H, W, C, heads;
+  WinGeom win[2];  // block parity 0: no shift, 1: shift 3 (disabled per axis when 7 >= padded size)
+};
+
+struct SwinBlockW {
+  size_t n1w, n1b, qkvw, qkvb, projw, projb, table, n2w, n2b, fc1w, fc1b, fc2w, fc2b;
+};
+struct MergeW {
+  size_t nw, nb, redw;
+};
+struct DecLayerW {
+  size_t sa_inw, sa_inb, sa_ow, sa_ob, ca_inw, ca_inb, ca_ow, ca_ob, l1w, l1b, l2w, l2b, n1w, n1b, n2w, n2b, n3w,
+      n3b;
+};
+
+// Blob layout: the order of synth.py:param_specs.
+struct Layout {
+  size_t stem_w, stem_b, stem_lnw, stem_lnb;
+  std::vector<SwinBlockW> blocks;  // 12
+  MergeW merge[3];
+  size_t projw, projb, emb, pos;
+  std::vector<DecLayerW> layers;
+  size_t fcw, fcb;
+  size_t total;
+
+  explicit Layout(const mocr_config& c) {
+    size_t off = 0;
+    auto take = [&](size_t n) {
+      size_t o = off;
+      off += n;
+      return o;
+    };
+    const size_t d = c.d_model, ff = c.d_ff, V = c.vocab;
+    stem_w = take(kEmbed * 16);
+    stem_b = take(kEmbed);
+    stem_lnw = take(kEmbed);
+    stem_lnb = take(kEmbed);
+    size_t dim = kEmbed;
+    for (int s = 0; s < kStages; ++s) {
+      for (int j = 0; j < kDepth[s]; ++j) {
+        SwinBlockW b;
+        b.n1w = take(dim);
+        b.n1b = take(dim);
+        b.qkvw = take(3 * dim * dim);
+        b.qkvb = take(3 * dim);
+        b.projw = take(dim * dim);
+        b.projb = take(dim);
+        b.table = take(169 * (size_t)kHeads[s]);
+        b.n2w = take(dim);
+        b.n2b = take(dim);
+        b.fc1w = take(4 * dim * dim);
+        b.fc1b = take(4 * dim);
+        b.fc2w = take(4 * dim * dim);
+        b.fc2b = take(dim);
+        blocks.push_back(b);
+      }
+      if (s < kStages - 1) {
+        merge[s].nw = take(4 * dim);
+        merge[s].nb = take(4 * dim);
+        merge[s].redw = take(8 * dim * dim);
+        dim *= 2;
+      }
+    }
+    projw = take(d * kEncDim);
+    projb = take(d);
+    emb = take(V * d);
+    pos = take((size_t)c.max_pos * d);
+    for (int l = 0; l < c.n_layers; ++l) {
+      DecLayerW w;
+      w.sa_inw = take(3 * d * d);
+      w.sa_inb = take(3 * d);
+      w.sa_ow = take(d * d);
+      w.sa_ob = take(d);
+      w.ca_inw = take(3 * d * d);
+      w.ca_inb = take(3 * d);
+      w.ca_ow = take(d * d);
+      w.ca_ob = take(d);
+      w.l1w = take(ff * d);
+      w.l1b = take(ff);
+      w.l2w = take(d * ff);
+      w.l2b = take(d);
+      w.n1w = take(d);
+      w.n1b = take(d);
+      w.n2w = take(d);
+      w.n2b = take(d);
+      w.n3w = take(d);
+      w.n3b = take(d);
+      layers.push_back(w);
+    }
+    fcw = take(V * d);
+    fcb = take(V);
+    total = off;
+  }
+};
+
+void check_config(const mocr_config& c) {
+  auto req = [](bool ok, const char* what) {
+    if (!ok) throw std::runtime_error(std::string("invalid config: ") + what);
+  };
+  req(c.img_h >= 4 && c.img_w >= 4, "image smaller than one patch");
+  req(c.vocab > 0, "vocab");
+  req(c.d_model == 256 && c.n_heads == 8, "decoder kernels are built for d_model=256, 8 heads");
+  req(c.d_ff == 512, "decoder kernels are built for d_ff=512");
+  req(c.n_layers >= 1 && c.n_layers <= 64, "n_layers");
+  req(c.max_pos >= 2 && c.max_pos <= 256, "max_pos in [2,256]");
+  req(c.max_batch >= 1 && c.max_batch <= 4096, "max_batch");
+  req(c.precision == MOCR_PRECISION_FP32 || c.precision == MOCR_PRECISION_BF16, "precision");
+  req(c.sos_id >= 0 && c.sos_id < c.vocab && c.eos_id >= 0 && c.eos_id < c.vocab, "special ids");
+}
+
+StageGeom make_win(int H, int W, int C, int heads) {
+  StageGeom g{};
+  g.H = H;
+  g.W = W;
+  g.C = C;
+  g.heads = heads;
+  for (int par = 0; par < 2; ++par) {
+    WinGeom& w = g.win[par];
+    w.H = H;
+    w.W = W;
+    w.pH = (H + kWin - 1) / kWin * kWin;
+    w.pW = (W + kWin - 1) / kWin * kWin;
+    const int shift = par ? kWin / 2 : 0;
+    w.sh = (kWin >= w.pH) ? 0 : shift;
+    w.sw = (kWin >= w.pW) ? 0 : shift;
+    w.nWx = w.pW / kWin;
+    w.nWin = (w.pH / kWin) * w.nWx;
+  }
+  return g;
+}
+
+template <typename T>
+T* dalloc(size_t n) {
+  void* p = nullptr;
+  if (n == 0) n = 1;
+  MOCR_HIP_CHECK(hipMalloc(&p, n * sizeof(T)));
+  return static_cast<T*>(p);
+}
+
+struct TimingRec {
+  std::string name;
+  hipEvent_t e0, e1;
+  double flops, bytes;
+};
+
+}  // namespace
+
+struct mocr_engine {
+  mocr_config cfg{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  std::unique_ptr<Layout> lay;
+
+  // geometry
+  int H1 = 0, W1 = 0, Hm = 0, Wm = 0, M = 0, Vpad = 0;
+  StageGeom stage[kStages];
+
+  // weights
+  float* dw = nullptr;
+  std::vector<float*> relbias;  // per Swin block [heads,49,49]
+  float* fcw_pad = nullptr;
+  float* fcb_pad = nullptr;
+  float* kvw_all = nullptr;  // [L*2d, d] cross-attention k/v in_proj rows of every layer
+  float* kvb_all = nullptr;
+  bool weights_loaded = false;
+
+  // encoder activations
+  float *img = nullptr, *X = nullptr, *X2 = nullptr, *XW = nullptr, *QKV = nullptr, *ATT = nullptr, *HID = nullptr;
+  float *MEM = nullptr, *MEMKV = nullptr;
+  size_t szX = 0, szXW = 0, szQKV = 0, szHID = 0;
+  int cur_batch = 0;
+  bool encoded = false;
+  int partial_stage = -1;
+
+  // decoder state
+  float *dx = nullptr, *dq = nullptr, *datt = nullptr, *dy = nullptr, *dh = nullptr, *dlogits = nullptr;
+  float* dlogits_hist = nullptr;
+  float *kcache = nullptr, *vcache = nullptr;
+  int32_t *ids = nullptr, *feed = nullptr, *forced = nullptr, *finished = nullptr;
+  float* logp = nullptr;
+  DecodeState* st = nullptr;
+  int ld_ids = 0;
+  std::map<std::tuple<int, int, int>, hipGraphExec_t> graphs;
+
+  // timing
+  bool timing = false;
+  std::vector<TimingRec> pending;
+  std::map<std::string, mocr_kernel_stat> stats;
+  std::vector<hipEvent_t> event_pool;
+
+  ~mocr_engine() {
+    (void)hipSetDevice(device);
+    for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+    for (auto e : event_pool) (void)hipEventDestroy(e);
+    for (auto& r : pending) {
+      (void)hipEventDestroy(r.e0);
+      (void)hipEventDestroy(r.e1);
+    }
+    void* bufs[] = {dw,      fcw_pad, fcb_pad, kvw_all, kvb_all, img,  X,        X2,       XW,     QKV,
+                    ATT,     HID,     MEM,     MEMKV,   dx,      dq,   datt,     dy,       dh,     dlogits,
+                    dlogits_hist, kcache, vcache, ids, feed, forced, finished, logp, st};
+    for (void* p : bufs)
+      if (p) (void)hipFree(p);
+    for (float* p : relbias)
+      if (p) (void)hipFree(p);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  const float* W(size_t off) const { return dw + off; }
+
+  // ---------------------------------------------------------------- setup
+  void init(const mocr_config& c, int dev) {
+    check_config(c);
+    cfg = c;
+    device = dev;
+    MOCR_HIP_CHECK(hipSetDevice(device));
+    MOCR_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    lay.reset(new Layout(cfg));
+
+    H1 = cfg.img_h / 4;
+    W1 = cfg.img_w / 4;
+    int H = H1, Wd = W1, C = kEmbed;
+    const size_t B = cfg.max_batch;
+    for (int s = 0; s < kStages; ++s) {
+      stage[s] = make_win(H, Wd, C, kHeads[s]);
+      const WinGeom& wg = stage[s].win[0];
+      szX = std::max(szX, B * H * Wd * C);
+      szXW = std::max(szXW, B * wg.nWin * kWinTok * C);
+      szQKV = std::max(szQKV, B * wg.nWin * kWinTok * 3 * C);
+      szHID = std::max(szHID, B * H * Wd * 4 * C);
+      if (s < kStages - 1) {
+        const int Ho = (H + 1) / 2, Wo = (Wd + 1) / 2;
+        szXW = std::max(szXW, B * Ho * Wo * 4 * C);
+        szX = std::max(szX, B * Ho * Wo * 2 * C);
+        H = Ho;
+        Wd = Wo;
+        C *= 2;
+      }
+    }
+    Hm = H;
+    Wm = Wd;
+    M = Hm * Wm;
+    Vpad = (cfg.vocab + 15) / 16 * 16;
+    const size_t d = cfg.d_model, L = cfg.n_layers;
+
+    dw = dalloc<float>(lay->total);
+    relbias.assign(lay->blocks.size(), nullptr);
+    for (size_t i = 0, bi = 0; i < (size_t)kStages; ++i)
+      for (int j = 0; j < kDepth[i]; ++j, ++bi) relbias[bi] = dalloc<float>((size_t)kHeads[i] * kWinTok * kWinTok);
+    fcw_pad = dalloc<float>((size_t)Vpad * d);
+    fcb_pad = dalloc<float>(Vpad);
+    kvw_all = dalloc<float>(L * 2 * d * d);
+    kvb_all = dalloc<float>(L * 2 * d);
+
+    img = dalloc<float>(B * cfg.img_h * cfg.img_w);
+    X = dalloc<float>(szX);
+    X2 = dalloc<float>(szX);
+    XW = dalloc<float>(szXW);
+    ATT = dalloc<float>(szXW);
+    QKV = dalloc<float>(szQKV);
+    HID = dalloc<float>(szHID);
+    MEM = dalloc<float>(B * M * d);
+    MEMKV = dalloc<float>(B * M * L * 2 * d);
+
+    dx = dalloc<float>(B * d);
+    dq = dalloc<float>(B * d);
+    datt = dalloc<float>(B * d);
+    dy = dalloc<float>(B * d);
+    dh = dalloc<float>(B * cfg.d_ff);
+    dlogits = dalloc<float>(B * Vpad);
+    kcache = dalloc<float>(L * B * cfg.max_pos * d);
+    vcache = dalloc<float>(L * B * cfg.max_pos * d);
+    ld_ids = cfg.max_pos + 1;
+    ids = dalloc<int32_t>(B * ld_ids);
+    feed = dalloc<int32_t>(B * ld_ids);
+    forced = dalloc<int32_t>(B * ld_ids);
+    finished = dalloc<int32_t>(B);
+    logp = dalloc<float>(B * cfg.max_pos);
+    st = dalloc<DecodeState>(1);
+  }
+
+  void load_weights(const float* blob, size_t n) {
+    if (n != lay->total)
+      throw std::runtime_error("weight blob has " + std::to_string(n) + " floats, expected " +
+                               std::to_string(lay->total));
+    MOCR_HIP_CHECK(hipSetDevice(device));
+    MOCR_HIP_CHECK(hipMemcpy(dw, blob, n * sizeof(float), hipMemcpyHostToDevice));
+    // Expanded relative-position bias [h, 49, 49] = table[index(i, j), h]
+    // (torchvision _get_relative_position_bias with relative_position_index).
+    size_t bi = 0;
+    for (int s = 0; s < kStages; ++s) {
+      const int h = kHeads[s];
+      for (int j = 0; j < kDepth[s]; ++j, ++bi) {
+        const float* table = blob + lay->blocks[bi].table;
+        std::vector<float> rb((size_t)h * kWinTok * kWinTok);
+        for (int i = 0; i < kWinTok; ++i)
+          for (int k = 0; k < kWinTok; ++k) {
+            const int dy = i / kWin - k / kWin + kWin - 1;
+            const int dx = i % kWin - k % kWin + kWin - 1;
+            const int idx = dy * (2 * kWin - 1) + dx;
+            for (int hh = 0; hh < h; ++hh) rb[((size_t)hh * kWinTok + i) * kWinTok + k] = table[idx * h + hh];
+          }
+        MOCR_HIP_CHECK(hipMemcpy(relbias[bi], rb.data(), rb.size() * sizeof(float), hipMemcpyHostToDevice));
+      }
+    }
+    const size_t d = cfg.d_model, V = cfg.vocab;
+    MOCR_HIP_CHECK(hipMemset(fcw_pad, 0, (size_t)Vpad * d * sizeof(float)));
+    MOCR_HIP_CHECK(hipMemset(fcb_pad, 0, (size_t)Vpad * sizeof(float)));
+    MOCR_HIP_CHECK(hipMemcpy(fcw_pad, dw + lay->fcw, V * d * sizeof(float), hipMemcpyDeviceToDevice));
+    MOCR_HIP_CHECK(hipMemcpy(fcb_pad, dw + lay->fcb, V * sizeof(float), hipMemcpyDeviceToDevice));
+    for (int l = 0; l < cfg.n_layers; ++l) {
+      const DecLayerW& w = lay->layers[l];
+      MOCR_HIP_CHECK(hipMemcpy(kvw_all + (size_t)l * 2 * d * d, dw + w.ca_inw + d * d, 2 * d * d * sizeof(float),
+                               hipMemcpyDeviceToDevice));
+      MOCR_HIP_CHECK(hipMemcpy(kvb_all + (size_t)l * 2 * d, dw + w.ca_inb + d, 2 * d * sizeof(float),
+                               hipMemcpyDeviceToDevice));
+    }
+    MOCR_HIP_CHECK(hipDeviceSynchronize());
+    weights_loaded = true;
+    encoded = false;
+  }
+
+  void set_images(const float* src, int B, hipMemcpyKind kind) {
+    if (B < 1 || B > cfg.max_batch) throw std::runtime_error("batch must be in [1, max_batch]");
+    MOCR_HIP_CHECK(hipSetDevice(device));
+    MOCR_HIP_CHECK(
+        hipMemcpyAsync(img, src, (size_t)B * cfg.img_h * cfg.img_w * sizeof(float), kind, stream));
+    MOCR_HIP_CHECK(hipStreamSynchronize(stream));
+    cur_batch = B;
+    encoded = false;
+  }
+
+  // ---------------------------------------------------------------- timing
+  hipEvent_t get_event() {
+    if (!event_pool.empty()) {
+      hipEvent_t e = event_pool.back();
+      event_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    MOCR_HIP_CHECK(hipEventCreate(&e));
+    return e;
+  }
+
+  template <typename F>
+  void timed(const char* name, double flops, double bytes, F&& f) {
+    if (!timing) {
+      f();
+      return;
+    }
+    TimingRec r{name, get_event(), get_event(), flops, bytes};
+    MOCR_HIP_CHECK(hipEventRecord(r.e0, stream));
+    f();
+    MOCR_HIP_CHECK(hipEventRecord(r.e1, stream));
+    pending.push_back(r);
+  }
+
+  void flush_timing() {
+    for (auto& r : pending) {
+      MOCR_HIP_CHECK(hipEventSynchronize(r.e1));
+      float ms = 0.f;
+      MOCR_HIP_CHECK(hipEventElapsedTime(&ms, r.e0, r.e1));
+      mocr_kernel_stat& s = stats[r.name];
+      std::strncpy(s.name, r.name.c_str(), sizeof(s.name) - 1);
+      s.launches += 1;
+      s.total_ms += ms;
+      s.flops += r.flops;
+      s.bytes += r.bytes;
+      event_pool.push_back(r.e0);
+      event_pool.push_back(r.e1);
+    }
+    pending.clear();
+  }
+
+  // ---------------------------------------------------------------- encoder
+  void gemm(const char* name, const float* A, const float* Wt, const float* bias, float* C, int Mrows, int N, int K,
+            int epi, const WinGeom* wg, long alg_rows) {
+    GemmParams p{};
+    p.A = A;
+    p.W = Wt;
+    p.bias = bias;
+    p.C = C;
+    p.M = Mrows;
+    p.N = N;
+    p.K = K;
+    p.lda = K;
+    p.ldw = K;
+    p.ldc = N;
+    p.epi = epi;
+    if (wg) p.win = *wg;
+    const double flops = 2.0 * alg_rows * N * K;
+    const double bytes = 4.0 * ((double)alg_rows * K + (double)N * K + (double)alg_rows * N *
+                                                                            (epi == EPI_RESADD || epi == EPI_WINRES ? 2 : 1));
+    timed(name, flops, bytes, [&] { launch_gemm_f32(p, stream); });
+  }
+
+  // stop_after = k >= 0 stops after features[k] (0 = stem, 1..7 = stages/merges) and leaves
+  // that NHWC map in X (parity debugging); -1 runs the whole encoder.
+  void encode(int B, int stop_after = -1) {
+    if (!weights_loaded) throw std::runtime_error("weights not loaded");
+    if (B != cur_batch) throw std::runtime_error("batch differs from the uploaded images");
+    if (cfg.precision != MOCR_PRECISION_FP32) throw std::runtime_error("bf16 precision is not built yet");
+    MOCR_HIP_CHECK(hipSetDevice(device));
+    const size_t d = cfg.d_model, L = cfg.n_layers;
+    timed("stem", 2.0 * B * H1 * W1 * kEmbed * 16, 4.0 * B * (cfg.img_h * cfg.img_w + (double)H1 * W1 * kEmbed),
+          [&] { launch_stem(img, W(lay->stem_w), W(lay->stem_b), W(lay->stem_lnw), W(lay->stem_lnb), X, B,
+                            cfg.img_h, cfg.img_w, stream); });
+    if (stop_after == 0) return finish_partial(0);
+    size_t bi = 0;
+    static const char* qkv_n[] = {"s1.qkv", "s2.qkv", "s3.qkv", "s4.qkv"};
+    static const char* proj_n[] = {"s1.proj", "s2.proj", "s3.proj", "s4.proj"};
+    static const char* fc1_n[] = {"s1.fc1", "s2.fc1", "s3.fc1", "s4.fc1"};
+    static const char* fc2_n[] = {"s1.fc2", "s2.fc2", "s3.fc2", "s4.fc2"};
+    static const char* att_n[] = {"s1.wattn", "s2.wattn", "s3.wattn", "s4.wattn"};
+    static const char* mrg_n[] = {"merge1", "merge2", "merge3"};
+    for (int s = 0; s < kStages; ++s) {
+      const StageGeom& g = stage[s];
+      const int C = g.C;
+      const long rows = (long)B * g.H * g.W;
+      for (int j = 0; j < kDepth[s]; ++j, ++bi) {
+        const SwinBlockW& w = lay->blocks[bi];
+        const WinGeom& wg = g.win[j & 1];
+        const long wrows = (long)B * wg.nWin * kWinTok;
+        launch_ln_partition(X, W(w.n1w), W(w.n1b), XW, nullptr, B, C, wg, stream);
+        gemm(qkv_n[s], XW, W(w.qkvw), W(w.qkvb), QKV, (int)wrows, 3 * C, C, EPI_STORE, nullptr, rows);
+        timed(att_n[s], 4.0 * rows * kWinTok * C, 4.0 * (double)rows * 4 * C,
+              [&] { launch_window_attention(QKV, relbias[bi], ATT, nullptr, B, C, g.heads, wg, stream); });
+        gemm(proj_n[s], ATT, W(w.projw), W(w.projb), X, (int)wrows, C, C, EPI_WINRES, &wg, rows);
+        launch_layernorm(X, W(w.n2w), W(w.n2b), XW, nullptr, (int)rows, C, stream);
+        gemm(fc1_n[s], XW, W(w.fc1w), W(w.fc1b), HID, (int)rows, 4 * C, C, EPI_GELU, nullptr, rows);
+        gemm(fc2_n[s], HID, W(w.fc2w), W(w.fc2b), X, (int)rows, C, 4 * C, EPI_RESADD, nullptr, rows);
+      }
+      if (stop_after == 1 + 2 * s) return finish_partial(1 + 2 * s);
+      if (s < kStages - 1) {
+        const MergeW& m = lay->merge[s];
+        const long orow = (long)B * ((g.H + 1) / 2) * ((g.W + 1) / 2);
+        launch_merge_ln(X, W(m.nw), W(m.nb), XW, nullptr, B, g.H, g.W, C, stream);
+        gemm(mrg_n[s], XW, W(m.redw), nullptr, X2, (int)orow, 2 * C, 4 * C, EPI_STORE, nullptr, orow);
+        std::swap(X, X2);
+        if (stop_after == 2 + 2 * s) return finish_partial(2 + 2 * s);
+      }
+    }
+    gemm("memproj", X, W(lay->projw), W(lay->projb), MEM, B * M, (int)d, kEncDim, EPI_STORE, nullptr, (long)B * M);
+    gemm("crosskv", MEM, kvw_all, kvb_all, MEMKV, B * M, (int)(L * 2 * d), (int)d, EPI_STORE, nullptr,
+         (long)B * M);
+    MOCR_HIP_CHECK(hipStreamSynchronize(stream));
+    if (timing) flush_timing();
+    encoded = true;
+  }
+
+  void finish_partial(int k) {
+    MOCR_HIP_CHECK(hipStreamSynchronize(stream));
+    if (timing) flush_timing();
+    partial_stage = k;
+    encoded = false;
+  }
+
+  size_t stage_elems(int k) const {
+    if (k == 0) return (size_t)cur_batch * stage[0].H * stage[0].W * stage[0].C;
+    const int s = (k - 1) / 2;
+    if (k % 2 == 1) return (size_t)cur_batch * stage[s].H * stage[s].W * stage[s].C;
+    return (size_t)cur_batch * stage[s + 1].H * stage[s + 1].W * stage[s + 1].C;
+  }
+
+  // ---------------------------------------------------------------- decoder
+  void record_step(int B, bool hist, bool use_forced) {
+    const int d = cfg.d_model, L = cfg.n_layers;
+    const size_t cache_layer = (size_t)cfg.max_batch * cfg.max_pos * d;
+    launch_dec_embed(st, feed, ld_ids, W(lay->emb), W(lay->pos), dx, B, d, stream);
+    for (int l = 0; l < L; ++l) {
+      const DecLayerW& w = lay->layers[l];
+      float* kc = kcache + l * cache_layer;
+      float* vc = vcache + l * cache_layer;
+      RowGemmParams p{};
+      p.B = B;
+      p.st = st;
+      p.d = d;
+      p.max_pos = cfg.max_pos;
+      // self-attention block (post-norm): x = norm1(x + SA(x))
+      p.A = dx; p.W = W(w.sa_inw); p.bias = W(w.sa_inb); p.out = dq; p.kcache = kc; p.vcache = vc;
+      p.N = 3 * d; p.K = d; p.ldo = d; p.n_valid = 3 * d; p.epi = DEC_QKV;
+      launch_rowgemm(p, stream);
+      launch_dec_self_attn(st, dq, kc, vc, datt, B, d, cfg.n_heads, cfg.max_pos, stream);
+      p.A = datt; p.W = W(w.sa_ow); p.bias = W(w.sa_ob); p.out = dy; p.resid = dx;
+      p.N = d; p.n_valid = d; p.epi = DEC_RESADD;
+      launch_rowgemm(p, stream);
+      launch_dec_layernorm(st, dy, W(w.n1w), W(w.n1b), dx, B, d, stream);
+      // cross-attention block: x = norm2(x + MHA(x, mem))
+      p.A = dx; p.W = W(w.ca_inw); p.bias = W(w.ca_inb); p.out = dq; p.resid = nullptr;
+      p.N = d; p.n_valid = d; p.epi = DEC_STORE;
+      launch_rowgemm(p, stream);
+      launch_dec_cross_attn(st, dq, MEMKV, L * 2 * d, l * 2 * d, l * 2 * d + d, datt, B, M, d, cfg.n_heads, stream);
+      p.A = datt; p.W = W(w.ca_ow); p.bias = W(w.ca_ob); p.out = dy; p.resid = dx;
+      p.N = d; p.n_valid = d; p.epi = DEC_RESADD;
+      launch_rowgemm(p, stream);
+      launch_dec_layernorm(st, dy, W(w.n2w), W(w.n2b), dx, B, d, stream);
+      // feed-forward block: x = norm3(x + W2 relu(W1 x))
+      p.A = dx; p.W = W(w.l1w); p.bias = W(w.l1b); p.out = dh; p.resid = nullptr;
+      p.N = cfg.d_ff; p.K = d; p.ldo = cfg.d_ff; p.n_valid = cfg.d_ff; p.epi = DEC_RELU;
+      launch_rowgemm(p, stream);
+      p.A = dh; p.W = W(w.l2w); p.bias = W(w.l2b); p.out = dy; p.resid = dx;
+      p.N = d; p.K = cfg.d_ff; p.ldo = d; p.n_valid = d; p.epi = DEC_RESADD;
+      launch_rowgemm(p, stream);
+      launch_dec_layernorm(st, dy, W(w.n3w), W(w.n3b), dx, B, d, stream);
+    }
+    RowGemmParams p{};
+    p.B = B;
+    p.st = st;
+    p.A = dx;
+    p.W = fcw_pad;
+    p.bias = fcb_pad;
+    p.out = hist ? dlogits_hist : dlogits;
+    p.hist_stride = hist ? (size_t)cfg.max_batch * Vpad : 0;
+    p.N = Vpad;
+    p.K = d;
+    p.ldo = Vpad;
+    p.n_valid = cfg.vocab;
+    p.epi = DEC_LOGITS;
+    launch_rowgemm(p, stream);
+    launch_dec_argmax(st, p.out, p.hist_stride, Vpad, cfg.vocab, B, ids, feed, use_forced ? forced : nullptr, ld_ids,
+                      logp, finished, cfg.eos_id, stream);
+  }
+
+  hipGraphExec_t graph_for(int B, bool hist, bool use_forced) {
+    auto key = std::make_tuple(B, (int)hist, (int)use_forced);
+    auto it = graphs.find(key);
+    if (it != graphs.end()) return it->second;
+    hipGraph_t g;
+    MOCR_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    try {
+      for (int i = 0; i < kDecodeChunk; ++i) record_step(B, hist, use_forced);
+    } catch (...) {
+      (void)hipStreamEndCapture(stream, &g);
+      throw;
+    }
+    MOCR_HIP_CHECK(hipStreamEndCapture(stream, &g));
+    hipGraphExec_t exec;
+    MOCR_HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
+    MOCR_HIP_CHECK(hipGraphDestroy(g));
+    graphs[key] = exec;
+    return exec;
+  }
+
+  // Runs the decode; returns steps run.
+  int decode(int max_steps, int stop_mode, const int32_t* forced_host, bool want_logits) {
+    if (!encoded) throw std::runtime_error("mocr_decode before mocr_encode");
+    if (max_steps < 1 || max_steps > cfg.max_pos) throw std::runtime_error("max_steps must be in [1, max_pos]");
+    if (stop_mode != MOCR_STOP_BATCH && stop_mode != MOCR_STOP_NONE) throw std::runtime_error("bad stop_mode");
+    MOCR_HIP_CHECK(hipSetDevice(device));
+    const int B = cur_batch;
+    if (want_logits && !dlogits_hist) dlogits_hist = dalloc<float>((size_t)cfg.max_pos * cfg.max_batch * Vpad);
+    // ids/feed: column 0 = sos, the rest pad (src/inference.py:15)
+    std::vector<int32_t> init((size_t)B * ld_ids, cfg.pad_id);
+    for (int b = 0; b < B; ++b) init[(size_t)b * ld_ids] = cfg.sos_id;
+    MOCR_HIP_CHECK(hipMemcpyAsync(ids, init.data(), init.size() * 4, hipMemcpyHostToDevice, stream));
+    if (forced_host) {
+      std::vector<int32_t> f((size_t)B * ld_ids, cfg.pad_id);
+      for (int b = 0; b < B; ++b)
+        std::memcpy(&f[(size_t)b * ld_ids], forced_host + (size_t)b * (max_steps + 1), (max_steps + 1) * 4);
+      MOCR_HIP_CHECK(hipMemcpyAsync(forced, f.data(), f.size() * 4, hipMemcpyHostToDevice, stream));
+      MOCR_HIP_CHECK(hipMemcpyAsync(feed, f.data(), f.size() * 4, hipMemcpyHostToDevice, stream));
+      MOCR_HIP_CHECK(hipStreamSynchronize(stream));
+    } else {
+      MOCR_HIP_CHECK(hipMemcpyAsync(feed, init.data(), init.size() * 4, hipMemcpyHostToDevice, stream));
+      MOCR_HIP_CHECK(hipStreamSynchronize(stream));
+    }
+    MOCR_HIP_CHECK(hipMemsetAsync(finished, 0, (size_t)B * 4, stream));
+    DecodeState h{};
+    h.t = -1;
+    h.max_steps = max_steps;
+    h.stop_mode = stop_mode;
+    MOCR_HIP_CHECK(hipMemcpyAsync(st, &h, sizeof(h), hipMemcpyHostToDevice, stream));
+    hipGraphExec_t exec = graph_for(B, want_logits, forced_host != nullptr);
+    const int chunks = (max_steps + kDecodeChunk - 1) / kDecodeChunk;
+    DecodeState hs{};
+    for (int c = 0; c < chunks; ++c) {
+      MOCR_HIP_CHECK(hipGraphLaunch(exec, stream));
+      if (stop_mode == MOCR_STOP_BATCH && c + 1 < chunks) {
+        MOCR_HIP_CHECK(hipMemcpyAsync(&hs, st, sizeof(hs), hipMemcpyDeviceToHost, stream));
+        MOCR_HIP_CHECK(hipStreamSynchronize(stream));
+        if (hs.done) break;
+      }
+    }
+    MOCR_HIP_CHECK(hipMemcpyAsync(&hs, st, sizeof(hs), hipMemcpyDeviceToHost, stream));
+    MOCR_HIP_CHECK(hipStreamSynchronize(stream));
+    return hs.done && hs.nsteps > 0 ? hs.nsteps : max_steps;
+  }
+
+  void copy_ids(int32_t* dst, int max_steps, hipMemcpyKind kind) {
+    MOCR_HIP_CHECK(hipMemcpy2DAsync(dst, (max_steps + 1) * 4, ids, ld_ids * 4, (max_steps + 1) * 4, cur_batch, kind,
+                                    stream));
+    MOCR_HIP_CHECK(hipStreamSynchronize(stream));
+  }
+};
+
+// ====================================================================== C-ABI
+namespace {
+
+int fail(mocr_engine* e, const std::exception& ex, int code = -1) {
+  if (e) e->err = ex.what();
+  g_last_error = ex.what();
+  if (auto* he = dynamic_cast<const HipError*>(&ex)) return -1000 - (int)he->code;
+  return code;
+}
+
+#define MOCR_API_BODY(eng, body)                   \
+  try {                                            \
+    if (!(eng)) throw std::runtime_error("null engine"); \
+    body;                                          \
+    return 0;                                      \
+  } catch (const std::exception& ex) {             \
+    return fail(eng, ex);                          \
+  }
+
+}  // namespace
+
+extern "C" {
+
+int mocr_abi_version(void) { return MOCR_ABI_VERSION; }
+
+size_t mocr_weight_count(const mocr_config* cfg) {
+  try {
+    check_config(*cfg);
+    return Layout(*cfg).total;
+  } catch (const std::exception& ex) {
+    g_last_error = ex.what();
+    return 0;
+  }
+}
+
+int mocr_memory_tokens(const mocr_config* cfg) {
+  int H = cfg->img_h / 4, W = cfg->img_w / 4;
+  for (int s = 0; s < kStages - 1; ++s) {
+    H = (H + 1) / 2;
+    W = (W + 1) / 2;
+  }
+  return H * W;
+}
+
+int mocr_create(const mocr_config* cfg, int hip_device, mocr_engine** out) {
+  mocr_engine* e = nullptr;
+  try {
+    if (!cfg || !out) throw std::runtime_error("null argument");
+    e = new mocr_engine();
+    e->init(*cfg, hip_device);
+    *out = e;
+    return 0;
+  } catch (const std::exception& ex) {
+    int rc = fail(nullptr, ex);
+    delete e;
+    if (out) *out = nullptr;
+    return rc;
+  }
+}
+
+int mocr_destroy(mocr_engine* eng) {
+  delete eng;
+  return 0;
+}
+
+const char* mocr_last_error(const mocr_engine* eng) { return eng ? eng->err.c_str() : g_last_error.c_str(); }
+
+int mocr_load_weights(mocr_engine* eng, const float* blob, size_t n) { MOCR_API_BODY(eng, eng->load_weights(blob, n)) }
+
+int mocr_set_images(mocr_engine* eng, const float* img_host, int batch) {
+  MOCR_API_BODY(eng, eng->set_images(img_host, batch, hipMemcpyHostToDevice))
+}
+
+int mocr_set_images_device(mocr_engine* eng, const float* img_dev, int batch) {
+  MOCR_API_BODY(eng, eng->set_images(img_dev, batch, hipMemcpyDeviceToDevice))
+}
+
+int mocr_encode(mocr_engine* eng, int batch) { MOCR_API_BODY(eng, eng->encode(batch)) }
+
+int mocr_get_memory(mocr_engine* eng, float* host_out) {
+  MOCR_API_BODY(eng, {
+    if (!eng->encoded) throw std::runtime_error("not encoded");
+    MOCR_HIP_CHECK(hipSetDevice(eng->device));
+    MOCR_HIP_CHECK(hipMemcpy(host_out, eng->MEM, (size_t)eng->cur_batch * eng->M * eng->cfg.d_model * sizeof(float),
+                             hipMemcpyDeviceToHost));
+  })
+}
+
+int mocr_decode(mocr_engine* eng, int max_steps, int stop_mode, const int32_t* forced_ids, int32_t* ids_out,
+                int32_t* n_steps_out, float* logp_out, float* logits_out) {
+  MOCR_API_BODY(eng, {
+    const int n = eng->decode(max_steps, stop_mode, forced_ids, logits_out != nullptr);
+    if (n_steps_out) *n_steps_out = n;
+    if (ids_out) eng->copy_ids(ids_out, max_steps, hipMemcpyDeviceToHost);
+    const int B = eng->cur_batch;
+    if (logp_out) {
+      MOCR_HIP_CHECK(hipMemcpy2D(logp_out, max_steps * 4, eng->logp, eng->cfg.max_pos * 4, max_steps * 4, B,
+                                 hipMemcpyDeviceToHost));
+    }
+    if (logits_out) {
+      const size_t V = eng->cfg.vocab;
+      for (int t = 0; t < max_steps; ++t) {
+        // hist slot t is [max_batch, Vpad]; out is [B, max_steps, V]
+        MOCR_HIP_CHECK(hipMemcpy2D(logits_out + (size_t)t * V, (size_t)max_steps * V * 4,
+                                   eng->dlogits_hist + (size_t)t * eng->cfg.max_batch * eng->Vpad,
+                                   (size_t)eng->Vpad * 4, V * 4, B, hipMemcpyDeviceToHost));
+      }
+    }
+  })
+}
+
+int mocr_decode_device(mocr_engine* eng, int max_steps, int stop_mode, int32_t* ids_dev, int32_t* n_steps_out) {
+  MOCR_API_BODY(eng, {
+    const int n = eng->decode(max_steps, stop_mode, nullptr, false);
+    if (n_steps_out) *n_steps_out = n;
+    eng->copy_ids(ids_dev, max_steps, hipMemcpyDeviceToDevice);
+  })
+}
+
+int mocr_debug_encode_until(mocr_engine* eng, int batch, int k, float* host_out, size_t n) {
+  MOCR_API_BODY(eng, {
+    if (k < 0 || k > 7) throw std::runtime_error("k must be in [0, 7]");
+    eng->encode(batch, k);
+    if (n != eng->stage_elems(k)) throw std::runtime_error("wrong output size for stage " + std::to_string(k));
+    MOCR_HIP_CHECK(hipMemcpy(host_out, eng->X, n * sizeof(float), hipMemcpyDeviceToHost));
+  })
+}
+
+int mocr_set_timing(mocr_engine* eng, int enabled) {
+  MOCR_API_BODY(eng, {
+    eng->timing = enabled != 0;
+    eng->stats.clear();
+  })
+}
+
+int mocr_get_timing(mocr_engine* eng, mocr_kernel_stat* out, int max_records) {
+  try {
+    if (!eng) throw std::runtime_error("null engine");
+    int n = 0;
+    for (auto& kv : eng->stats) {
+      if (n < max_records && out) out[n] = kv.second;
+      ++n;
+    }
+    return n;
+  } catch (const std::exception& ex) {
+    return fail(eng, ex);
+  }
+}
+
+}  // extern "C"

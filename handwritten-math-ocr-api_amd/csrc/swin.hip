@@ -1,0 +1,330 @@
+// Swin-T encoder kernels other than the GEMMs (torchvision swin_t().features, SURVEY.md
+// Appendix A; the 1-channel stem is src/model_swin.py:19-34).
+//
+// Activations are NHWC fp32 [B, H, W, C].  The shifted-window geometry (zero pad to a
+// multiple of 7 after norm1, roll(-s), window partition, region mask on the padded
+// map, window reverse, roll(+s), crop) is index arithmetic inside the kernels: the
+// padded/rolled map is never materialised.  Padded tokens enter the window as zero
+// rows after LayerNorm, so their k/v equal the qkv bias and they stay unmasked keys,
+// exactly as in torchvision.
+#include "kernels.h"
+
+namespace mocr {
+
+namespace {
+
+__device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// LayerNorm of one row held as NPER values per lane (element c = lane + 64*i), C valid.
+template <int NPER>
+__device__ __forceinline__ void ln_regs(float (&v)[NPER], int C, int lane, const float* g, const float* b) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPER; ++i)
+    if (lane + 64 * i < C) s += v[i];
+  const float mean = wave_sum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPER; ++i)
+    if (lane + 64 * i < C) {
+      const float d = v[i] - mean;
+      q += d * d;
+    }
+  const float var = wave_sum(q) / (float)C;
+  const float rstd = 1.0f / sqrtf(var + 1e-5f);
+#pragma unroll
+  for (int i = 0; i < NPER; ++i) {
+    const int c = lane + 64 * i;
+    if (c < C) v[i] = (v[i] - mean) * rstd * g[c] + b[c];
+  }
+}
+
+template <int NPER>
+__device__ __forceinline__ void store_row(float (&v)[NPER], int C, int lane, float* dst, uint16_t* dst16) {
+#pragma unroll
+  for (int i = 0; i < NPER; ++i) {
+    const int c = lane + 64 * i;
+    if (c < C) {
+      if (dst) dst[c] = v[i];
+      if (dst16) dst16[c] = f32_to_bf16_rne(v[i]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- stem
+// Conv2d(1, 96, k=4, s=4, bias) -> Permute -> LayerNorm(96).  One wave per output token.
+__global__ void __launch_bounds__(256) stem_kernel(const float* __restrict__ img, const float* __restrict__ w,
+                                                   const float* __restrict__ bias, const float* __restrict__ g,
+                                                   const float* __restrict__ beta, float* __restrict__ X, int B,
+                                                   int H, int W, int Hs, int Ws) {
+  const int lane = threadIdx.x & 63;
+  const long tok = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tok >= (long)B * Hs * Ws) return;
+  const int b = (int)(tok / (Hs * Ws));
+  const int rem = (int)(tok - (long)b * Hs * Ws);
+  const int y = rem / Ws;
+  const int x = rem - y * Ws;
+  float px[16];
+  const float* src = img + ((size_t)b * H + 4 * y) * W + 4 * x;
+#pragma unroll
+  for (int ky = 0; ky < 4; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 4; ++kx) px[ky * 4 + kx] = src[(size_t)ky * W + kx];
+  float v[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = lane + 64 * i;
+    float acc = 0.f;
+    if (c < 96) {
+      const float* wc = w + c * 16;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc = fmaf(wc[k], px[k], acc);
+      acc += bias[c];
+    }
+    v[i] = acc;
+  }
+  ln_regs<2>(v, 96, lane, g, beta);
+  store_row<2>(v, 96, lane, X + (size_t)tok * 96, nullptr);
+}
+
+// ---------------------------------------------------------------- LN + window partition
+template <int NPER>
+__global__ void __launch_bounds__(256) ln_partition_kernel(const float* __restrict__ X, const float* __restrict__ g,
+                                                           const float* __restrict__ b, float* __restrict__ XW,
+                                                           uint16_t* __restrict__ XW16, int B, int C, WinGeom wg) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int per_img = wg.nWin * kWinTok;
+  if (row >= (long)B * per_img) return;
+  const int bi = (int)(row / per_img);
+  const int rem = (int)(row - (long)bi * per_img);
+  const int win = rem / kWinTok;
+  const int tk = rem - win * kWinTok;
+  const int wy = win / wg.nWx;
+  const int wx = win - wy * wg.nWx;
+  int y = wy * kWin + tk / kWin + wg.sh;
+  int x = wx * kWin + tk % kWin + wg.sw;
+  if (y >= wg.pH) y -= wg.pH;
+  if (x >= wg.pW) x -= wg.pW;
+  float v[NPER];
+  float* dst = XW ? XW + (size_t)row * C : nullptr;
+  uint16_t* dst16 = XW16 ? XW16 + (size_t)row * C : nullptr;
+  if (y < wg.H && x < wg.W) {
+    const float* src = X + ((size_t)(bi * wg.H + y) * wg.W + x) * C;
+#pragma unroll
+    for (int i = 0; i < NPER; ++i) {
+      const int c = lane + 64 * i;
+      v[i] = c < C ? src[c] : 0.f;
+    }
+    ln_regs<NPER>(v, C, lane, g, b);
+  } else {
+#pragma unroll
+    for (int i = 0; i < NPER; ++i) v[i] = 0.f;  // F.pad after norm1: zero tokens
+  }
+  store_row<NPER>(v, C, lane, dst, dst16);
+}
+
+template <int NPER>
+__global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict__ X, const float* __restrict__ g,
+                                                        const float* __restrict__ b, float* __restrict__ Y,
+                                                        uint16_t* __restrict__ Y16, long rows, int C) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* src = X + (size_t)row * C;
+  float v[NPER];
+#pragma unroll
+  for (int i = 0; i < NPER; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < C ? src[c] : 0.f;
+  }
+  ln_regs<NPER>(v, C, lane, g, b);
+  store_row<NPER>(v, C, lane, Y ? Y + (size_t)row * C : nullptr, Y16 ? Y16 + (size_t)row * C : nullptr);
+}
+
+// ---------------------------------------------------------------- PatchMerging + LN(4C)
+template <int NPER>
+__global__ void __launch_bounds__(256) merge_ln_kernel(const float* __restrict__ X, const float* __restrict__ g,
+                                                       const float* __restrict__ b, float* __restrict__ Y,
+                                                       uint16_t* __restrict__ Y16, int B, int H, int W, int C) {
+  const int lane = threadIdx.x & 63;
+  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (long)B * Ho * Wo) return;
+  const int bi = (int)(row / (Ho * Wo));
+  const int rem = (int)(row - (long)bi * Ho * Wo);
+  const int oy = rem / Wo;
+  const int ox = rem - oy * Wo;
+  const int C4 = 4 * C;
+  float v[NPER];
+#pragma unroll
+  for (int i = 0; i < NPER; ++i) {
+    const int c4 = lane + 64 * i;
+    float val = 0.f;
+    if (c4 < C4) {
+      const int q = c4 / C;          // cat order x0=(0,0), x1=(1,0), x2=(0,1), x3=(1,1) as (dy,dx)
+      const int c = c4 - q * C;
+      const int y = 2 * oy + (q & 1);
+      const int x = 2 * ox + (q >> 1);
+      if (y < H && x < W) val = X[((size_t)(bi * H + y) * W + x) * C + c];
+    }
+    v[i] = val;
+  }
+  ln_regs<NPER>(v, C4, lane, g, b);
+  store_row<NPER>(v, C4, lane, Y ? Y + (size_t)row * C4 : nullptr, Y16 ? Y16 + (size_t)row * C4 : nullptr);
+}
+
+// ---------------------------------------------------------------- window attention
+// One workgroup per (window, head): Q/K/V 49x32 tiles staged in LDS, scores
+// (q*scale)·kᵀ + relative-position bias (+ -100 shift mask), row softmax with a
+// wave-wide max/sum reduce, then P·V.  q is scaled before the matmul and the mask is
+// added after the bias, as in torchvision.
+constexpr int QK_LD = kHeadDim + 1;
+constexpr int S_LD = kWinTok + 1;
+
+__global__ void __launch_bounds__(256) window_attention_kernel(const float* __restrict__ QKV,
+                                                               const float* __restrict__ relbias,
+                                                               float* __restrict__ O, uint16_t* __restrict__ O16,
+                                                               int C, WinGeom wg) {
+  __shared__ float q[kWinTok * QK_LD];
+  __shared__ float k[kWinTok * QK_LD];
+  __shared__ float v[kWinTok * kHeadDim];
+  __shared__ float S[kWinTok * S_LD];
+  __shared__ int region[kWinTok];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const long wg_idx = blockIdx.x;   // global window index (b * nWin + win)
+  const int h = blockIdx.y;
+  const int C3 = 3 * C;
+  const size_t base = (size_t)wg_idx * kWinTok;
+  const float scale = 0.17677669529663687f;  // 32 ** -0.5
+
+  for (int idx = tid; idx < kWinTok * kHeadDim; idx += 256) {
+    const int t = idx >> 5;
+    const int d = idx & 31;
+    const float* r = QKV + (base + t) * C3 + h * kHeadDim + d;
+    q[t * QK_LD + d] = r[0] * scale;
+    k[t * QK_LD + d] = r[C];
+    v[t * kHeadDim + d] = r[2 * C];
+  }
+  const bool masked = (wg.sh + wg.sw) > 0;
+  if (masked && tid < kWinTok) {
+    const int win = (int)(wg_idx % wg.nWin);
+    const int wy = win / wg.nWx;
+    const int wx = win - wy * wg.nWx;
+    const int py = wy * kWin + tid / kWin;
+    const int px = wx * kWin + tid % kWin;
+    region[tid] = 3 * shift_region(py, wg.pH, wg.sh) + shift_region(px, wg.pW, wg.sw);
+  }
+  __syncthreads();
+
+  const float* rb = relbias + (size_t)h * kWinTok * kWinTok;
+  for (int idx = tid; idx < kWinTok * kWinTok; idx += 256) {
+    const int i = idx / kWinTok;
+    const int j = idx - i * kWinTok;
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < kHeadDim; ++d) s = fmaf(q[i * QK_LD + d], k[j * QK_LD + d], s);
+    s = s + rb[idx];
+    if (masked && region[i] != region[j]) s = s + (-100.0f);
+    S[i * S_LD + j] = s;
+  }
+  __syncthreads();
+
+  for (int i = wave; i < kWinTok; i += 4) {
+    const float x = lane < kWinTok ? S[i * S_LD + lane] : -INFINITY;
+    const float m = wave_max(x);
+    const float e = lane < kWinTok ? expf(x - m) : 0.f;
+    const float sum = wave_sum(e);
+    if (lane < kWinTok) S[i * S_LD + lane] = e / sum;
+  }
+  __syncthreads();
+
+  for (int idx = tid; idx < kWinTok * kHeadDim; idx += 256) {
+    const int i = idx >> 5;
+    const int d = idx & 31;
+    float o = 0.f;
+#pragma unroll 7
+    for (int j = 0; j < kWinTok; ++j) o = fmaf(S[i * S_LD + j], v[j * kHeadDim + d], o);
+    const size_t off = (base + i) * C + h * kHeadDim + d;
+    if (O) O[off] = o;
+    if (O16) O16[off] = f32_to_bf16_rne(o);
+  }
+}
+
+__global__ void f32_to_bf16_kernel(const float* __restrict__ x, uint16_t* __restrict__ y, size_t n) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) y[i] = f32_to_bf16_rne(x[i]);
+}
+
+inline unsigned blocks_for_rows(long rows) { return (unsigned)((rows + 3) / 4); }
+
+}  // namespace
+
+void launch_stem(const float* img, const float* w, const float* b, const float* ln_w, const float* ln_b, float* X,
+                 int B, int H, int W, hipStream_t s) {
+  const int Hs = H / 4, Ws = W / 4;
+  stem_kernel<<<blocks_for_rows((long)B * Hs * Ws), 256, 0, s>>>(img, w, b, ln_w, ln_b, X, B, H, W, Hs, Ws);
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_ln_partition(const float* X, const float* g, const float* b, float* XW, uint16_t* XW16, int B, int C,
+                         const WinGeom& wg, hipStream_t s) {
+  const long rows = (long)B * wg.nWin * kWinTok;
+  switch ((C + 63) / 64) {
+    case 2: ln_partition_kernel<2><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, XW, XW16, B, C, wg); break;
+    case 3: ln_partition_kernel<3><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, XW, XW16, B, C, wg); break;
+    case 6: ln_partition_kernel<6><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, XW, XW16, B, C, wg); break;
+    case 12: ln_partition_kernel<12><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, XW, XW16, B, C, wg); break;
+    default: throw std::runtime_error("ln_partition: unsupported C " + std::to_string(C));
+  }
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_layernorm(const float* X, const float* g, const float* b, float* Y, uint16_t* Y16, int rows, int C,
+                      hipStream_t s) {
+  switch ((C + 63) / 64) {
+    case 2: layernorm_kernel<2><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, Y, Y16, rows, C); break;
+    case 3: layernorm_kernel<3><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, Y, Y16, rows, C); break;
+    case 4: layernorm_kernel<4><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, Y, Y16, rows, C); break;
+    case 6: layernorm_kernel<6><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, Y, Y16, rows, C); break;
+    case 12: layernorm_kernel<12><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, Y, Y16, rows, C); break;
+    default: throw std::runtime_error("layernorm: unsupported C " + std::to_string(C));
+  }
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_merge_ln(const float* X, const float* g, const float* b, float* Y, uint16_t* Y16, int B, int H, int W,
+                     int C, hipStream_t s) {
+  const long rows = (long)B * ((H + 1) / 2) * ((W + 1) / 2);
+  switch ((4 * C + 63) / 64) {
+    case 6: merge_ln_kernel<6><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, Y, Y16, B, H, W, C); break;
+    case 12: merge_ln_kernel<12><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, Y, Y16, B, H, W, C); break;
+    case 24: merge_ln_kernel<24><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, Y, Y16, B, H, W, C); break;
+    default: throw std::runtime_error("merge_ln: unsupported C " + std::to_string(C));
+  }
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_window_attention(const float* QKV, const float* relbias, float* O, uint16_t* O16, int B, int C,
+                             int heads, const WinGeom& wg, hipStream_t s) {
+  dim3 grid((unsigned)((long)B * wg.nWin), (unsigned)heads);
+  window_attention_kernel<<<grid, 256, 0, s>>>(QKV, relbias, O, O16, C, wg);
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_f32_to_bf16(const float* x, uint16_t* y, size_t n, hipStream_t s) {
+  if (n == 0) return;
+  const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 65536);
+  f32_to_bf16_kernel<<<blocks, 256, 0, s>>>(x, y, n);
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace mocr

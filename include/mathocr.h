@@ -1,0 +1,139 @@
+/*
+ * mathocr.h — C-ABI of libmathocr.so, the MI355X (gfx950) engine for the
+ * Swin-T encoder + 8-layer Transformer decoder greedy-decode hot path of
+ * PTD504/handwritten-math-ocr-api.
+ *
+ * The reference has no FFI for this path: its boundary is two Python calls that
+ * FastAPI consumes.  These entry points replace them:
+ *
+ *   app/src/im2latex.py:7    load_model(path, vocab, device)            -> mocr_create + mocr_load_weights
+ *   app/src/im2latex.py:15   predict(model, image[1,1,H,W], ...)        -> mocr_set_images + mocr_encode
+ *                                                                          + mocr_decode(stop_mode=MOCR_STOP_BATCH, logp_out)
+ *   src/inference.py:7       predict(images[B,1,H,W], model, ...)       -> mocr_set_images + mocr_encode
+ *                                                                          + mocr_decode(stop_mode=MOCR_STOP_BATCH)
+ *   src/model_swin.py:39-46  EncoderSwin.forward                        -> mocr_encode (+ mocr_get_memory)
+ *   src/model_swin.py:72-88  DecoderTransformer.forward (per step)      -> one step of mocr_decode
+ *
+ * The Python host layer (handwritten-math-ocr-api_amd/engine.py) binds these with
+ * ctypes and mirrors the reference's call signatures; see INTEGRATION.md.
+ *
+ * Conventions
+ *  - Every function returns 0 on success and a negative code on failure; the
+ *    message is in mocr_last_error(engine) (or mocr_last_error(NULL) for errors
+ *    raised before an engine exists).
+ *  - Host buffers are owned by the caller and are complete when the call returns
+ *    (all calls are synchronous).  Device buffers are owned by the engine, except
+ *    the *_device variants, which read/write caller-owned device memory on the
+ *    engine's device.
+ *  - One engine per device; calls on one engine must be serialised by the caller.
+ *    Calls release no locks of their own, so different engines may run in
+ *    different host threads concurrently.
+ */
+#ifndef MATHOCR_H_
+#define MATHOCR_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MOCR_ABI_VERSION 1
+
+/* Arithmetic of the engine. */
+enum {
+  MOCR_PRECISION_FP32 = 0, /* fp32 activations, fp32-input MFMA GEMMs: parity mode (token-exact) */
+  MOCR_PRECISION_BF16 = 1  /* bf16 MFMA encoder GEMMs with fp32 accumulate: throughput mode     */
+};
+
+/* Greedy stopping rule (src/inference.py:23-25). */
+enum {
+  MOCR_STOP_BATCH = 0, /* stop once every row has produced EOS (the reference); rows keep generating */
+  MOCR_STOP_NONE = 1   /* run exactly max_steps steps (bench: fixed work)                            */
+};
+
+typedef struct mocr_config {
+  int32_t img_h, img_w;  /* input image size, e.g. 384x384 (bench) or 96x320 (src/config.py:17-18) */
+  int32_t vocab;         /* V = 5075 for the published checkpoint                                  */
+  int32_t d_model;       /* 256  (src/config.py:19)                                                */
+  int32_t n_heads;       /* 8    (src/config.py:20)                                                */
+  int32_t d_ff;          /* 512  (src/config.py:21)                                                */
+  int32_t n_layers;      /* 8    (src/config.py:32)                                                */
+  int32_t max_pos;       /* 150  rows of the learned positional table (src/model_swin.py:54)       */
+  int32_t sos_id, eos_id, pad_id; /* 1, 2, 0 (src/utils.py:111)                                    */
+  int32_t max_batch;     /* device buffers are sized for this many images                          */
+  int32_t precision;     /* MOCR_PRECISION_*                                                       */
+} mocr_config;
+
+typedef struct mocr_engine mocr_engine;
+
+int mocr_abi_version(void);
+
+/* Number of float32 values mocr_load_weights expects for this config.  The blob
+ * is the concatenation, in order, of the tensors listed by
+ * handwritten-math-ocr-api_amd/synth.py:param_specs (reference state_dict names,
+ * encoder.features.* alias; relative_position_index buffers, decoder.tgt_mask
+ * and the unused swin.norm/head are not part of it). */
+size_t mocr_weight_count(const mocr_config* cfg);
+
+/* Encoder memory tokens per image: ceil-merged (H/4, W/4) map after 3 merges. */
+int mocr_memory_tokens(const mocr_config* cfg);
+
+int mocr_create(const mocr_config* cfg, int hip_device, mocr_engine** out);
+int mocr_destroy(mocr_engine* eng);
+const char* mocr_last_error(const mocr_engine* eng);
+
+/* Upload fp32 weights (host).  Derived tensors (expanded relative-position
+ * biases, bf16 copies, padded fc_out) are built on the device. */
+int mocr_load_weights(mocr_engine* eng, const float* blob, size_t n_floats);
+
+/* Images [B,1,H,W] fp32 NCHW in [-1,1] (app/src/preprocess.py:6-17) -> engine buffer. */
+int mocr_set_images(mocr_engine* eng, const float* img_host, int batch);
+int mocr_set_images_device(mocr_engine* eng, const float* img_dev, int batch);
+
+/* Encoder on the resident images: memory [B, M, d_model] and every layer's
+ * cross-attention K/V (computed once, not per step as in the reference). */
+int mocr_encode(mocr_engine* eng, int batch);
+
+/* Copy the encoder memory [B, M, d_model] fp32 to the host (parity tests). */
+int mocr_get_memory(mocr_engine* eng, float* host_out);
+
+/* Greedy decode of the encoded batch (src/inference.py:13-27).
+ *   forced_ids  nullable [B, max_steps+1]: teacher forcing — step t feeds
+ *               forced_ids[b][t] instead of the previous argmax (parity tests);
+ *   ids_out     [B, max_steps+1] int32, column 0 = sos; columns past *n_steps_out are pad;
+ *   n_steps_out number of steps run (< max_steps only with MOCR_STOP_BATCH);
+ *   logp_out    nullable [B, max_steps]: log(softmax(logits)[argmax] + 1e-10) per step
+ *               (app/src/im2latex.py:33-39);
+ *   logits_out  nullable [B, max_steps, vocab] fp32 last-position logits (parity only). */
+int mocr_decode(mocr_engine* eng, int max_steps, int stop_mode, const int32_t* forced_ids,
+                int32_t* ids_out, int32_t* n_steps_out, float* logp_out, float* logits_out);
+
+/* Same, ids written to caller device memory [B, max_steps+1] (e.g. a torch tensor
+ * that is then all-gathered over RCCL). */
+int mocr_decode_device(mocr_engine* eng, int max_steps, int stop_mode, int32_t* ids_dev,
+                       int32_t* n_steps_out);
+
+/* Parity debugging: run the encoder only up to torchvision features[k] (0 = stem,
+ * 1,3,5,7 = stages, 2,4,6 = PatchMerging) and copy that NHWC map (n floats) out. */
+int mocr_debug_encode_until(mocr_engine* eng, int batch, int k, float* host_out, size_t n);
+
+/* Per-kernel-class timing measured with HIP events on the engine stream while
+ * enabled (bench.py roofline).  Each record: {name, launches, total_ms, flops, bytes}. */
+typedef struct mocr_kernel_stat {
+  char name[48];
+  int64_t launches;
+  double total_ms;
+  double flops;  /* algorithmic FLOP summed over launches */
+  double bytes;  /* algorithmic HBM bytes summed over launches */
+} mocr_kernel_stat;
+
+int mocr_set_timing(mocr_engine* eng, int enabled); /* also resets the counters */
+int mocr_get_timing(mocr_engine* eng, mocr_kernel_stat* out, int max_records);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MATHOCR_H_ */
