@@ -42,17 +42,20 @@ __device__ __forceinline__ int shift_region(int y, int P, int s) {
   return (y >= P - kWin) + (y >= P - s);
 }
 
-// Step/stop state of a greedy decode, read by every decode kernel (device memory,
-// so one captured graph serves every step).
+// Batch-global stop state of a greedy decode (src/inference.py:23-25).  The step
+// index t is a kernel argument baked into the captured chunk graphs; kernels read
+// this only to skip steps after the batch has stopped: once every row has produced
+// EOS, done_step = the step of the last row's first EOS and later steps do nothing.
+// With stop_mode NONE the kernels get st = nullptr and never read it.
 struct DecodeState {
-  int t;          // index of the step being run (position of the fed token)
-  int done;       // 1 once the decode must stop (all rows finished or max_steps reached)
-  int nfinished;  // rows that have produced EOS
-  int nsteps;     // steps run when done
-  int max_steps;
-  int stop_mode;  // 0 = batch-global stop, 1 = none
-  int pad[2];
+  int done_step;    // INT_MAX until the batch has stopped
+  int nfinished;    // rows that have produced EOS
+  int last_finish;  // max over rows of the first-EOS step
+  int batch;
 };
+
+// True when step t must not write anything (read late, after the loads are issued).
+__device__ __forceinline__ bool dec_skip(const DecodeState* st, int t) { return st && t > st->done_step; }
 
 }  // namespace mocr
 

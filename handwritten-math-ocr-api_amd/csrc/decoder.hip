@@ -8,16 +8,26 @@
 // (gemm.hip).  With causal masking the newest position's output is the same
 // function of the same inputs.
 //
-// Every kernel reads the step index from DecodeState in device memory, so one
-// captured hipGraph of a step chunk is replayed for the whole decode; once the
-// batch has stopped (all rows hit EOS, or max_steps) every kernel exits at entry.
+// Post-norm LayerNorms are never materialised: a sublayer writes its pre-norm sum
+// y = x + f(x), and every consumer of LN(y) (the next projection's A operand, the
+// next residual) normalises the rows it reads, from row statistics it computes itself
+// with one fixed reduction order, so all consumers see bit-identical LN(y).
+//
+// The step index t is a kernel argument (one captured hipGraph per chunk of 8 steps);
+// no kernel reads device state before issuing its loads.  With the batch-global stop,
+// the stop flag is read alongside the loads and checked before the first store.
 #include "kernels.h"
 
 namespace mocr {
 
 namespace {
 
+constexpr int kD = 256;  // d_model (engine config is checked to match)
 constexpr float kAttnScale = 0.17677669529663687f;  // 1/sqrt(32)
+
+__device__ __forceinline__ float ln_apply(float v, float mean, float rstd, float g, float b) {
+  return fmaf((v - mean) * rstd, g, b);
+}
 
 // ------------------------------------------------------------------ small-M GEMM
 // out[B, N] = A[B, K] · W[N, K]^T + bias on v_mfma_f32_16x16x4_f32.  A workgroup
@@ -25,10 +35,47 @@ constexpr float kAttnScale = 0.17677669529663687f;  // 1/sqrt(32)
 // order.  Each lane loads float4 runs of A and W straight into registers (no reuse
 // inside the workgroup, so no LDS staging); lane group g = lane>>4 feeds
 // k = 4g + s at MFMA step s.
-template <int EPI, int KW>
+//
+// LN(A) / LN(resid) are fused: the 16 rows' statistics are reduced from fragments
+// that are already in registers (A's own fragments, or the resid rows loaded in the
+// same layout), two-pass mean / variance with a fixed order, so every consumer of a
+// LayerNorm gets bit-identical values.
+template <int NI>
+__device__ __forceinline__ void frag_ln_stats(const floatx4 (&f)[NI], float (*red)[16], int lane, int wave,
+                                              float& mean, float& rstd) {
+  const int row = lane & 15;
+  float ps = 0.f;
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) ps += f[i][s];
+  ps += __shfl_xor(ps, 16, 64);
+  ps += __shfl_xor(ps, 32, 64);
+  if (lane < 16) red[wave][row] = ps;
+  __syncthreads();
+  mean = (((red[0][row] + red[1][row]) + red[2][row]) + red[3][row]) * (1.0f / kD);
+  __syncthreads();
+  float pq = 0.f;
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const float t = f[i][s] - mean;
+      pq += t * t;
+    }
+  pq += __shfl_xor(pq, 16, 64);
+  pq += __shfl_xor(pq, 32, 64);
+  if (lane < 16) red[wave][row] = pq;
+  __syncthreads();
+  const float var = (((red[0][row] + red[1][row]) + red[2][row]) + red[3][row]) * (1.0f / kD);
+  rstd = 1.0f / sqrtf(var + 1e-5f);
+}
+
+template <int EPI, int KW, bool ALN, bool RLN>
 __global__ void __launch_bounds__(256) rowgemm_kernel(RowGemmParams p) {
-  if (p.st->done) return;
+  const int t = p.t;
   constexpr int NI = KW / 16;
+  constexpr int NR = kD / 4 / 16;  // resid fragments per lane (d split over 4 waves)
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -38,14 +85,50 @@ __global__ void __launch_bounds__(256) rowgemm_kernel(RowGemmParams p) {
   const int cb = c0 + (lane & 15);
   const int g = lane >> 4;
   const int kbeg = wave * KW;
+  const bool row_ok = ra < p.B;
 
   floatx4 a[NI], b[NI];
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     const int k = kbeg + i * 16 + 4 * g;
-    a[i] = ra < p.B ? *reinterpret_cast<const floatx4*>(p.A + (size_t)ra * p.K + k) : floatx4{0.f, 0.f, 0.f, 0.f};
+    a[i] = row_ok ? *reinterpret_cast<const floatx4*>(p.A + (size_t)ra * p.K + k) : floatx4{0.f, 0.f, 0.f, 0.f};
     b[i] = *reinterpret_cast<const floatx4*>(p.W + (size_t)cb * p.K + k);
   }
+  floatx4 rf[RLN ? NR : 1];
+  if constexpr (RLN) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int k = wave * (kD / 4) + i * 16 + 4 * g;
+      rf[i] = row_ok ? *reinterpret_cast<const floatx4*>(p.resid + (size_t)ra * p.ldo + k)
+                     : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+
+  __shared__ float red_s[4][16];
+  __shared__ float rn[16][kD + 1];
+  if constexpr (ALN) {
+    float mean, rstd;
+    frag_ln_stats<NI>(a, red_s, lane, wave, mean, rstd);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int k = kbeg + i * 16 + 4 * g;
+      const floatx4 gg = *reinterpret_cast<const floatx4*>(p.a_ln_g + k);
+      const floatx4 bb = *reinterpret_cast<const floatx4*>(p.a_ln_b + k);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) a[i][s] = row_ok ? ln_apply(a[i][s], mean, rstd, gg[s], bb[s]) : 0.f;
+    }
+  }
+  if constexpr (RLN) {
+    float mean, rstd;
+    frag_ln_stats<NR>(rf, red_s, lane, wave, mean, rstd);
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int k = wave * (kD / 4) + i * 16 + 4 * g;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) rn[lane & 15][k + s] = ln_apply(rf[i][s], mean, rstd, p.r_ln_g[k + s], p.r_ln_b[k + s]);
+    }
+  }
+
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < NI; ++i)
@@ -60,7 +143,7 @@ __global__ void __launch_bounds__(256) rowgemm_kernel(RowGemmParams p) {
   const int col = tid & 15;
   const int grow = r0 + row;
   const int gcol = c0 + col;
-  if (grow >= p.B || gcol >= p.n_valid) return;
+  if (grow >= p.B || gcol >= p.n_valid || dec_skip(p.st, t)) return;
   float v = ((red[0][row][col] + red[1][row][col]) + red[2][row][col]) + red[3][row][col];
   v += p.bias[gcol];
   if constexpr (EPI == DEC_STORE) {
@@ -68,9 +151,9 @@ __global__ void __launch_bounds__(256) rowgemm_kernel(RowGemmParams p) {
   } else if constexpr (EPI == DEC_RELU) {
     p.out[(size_t)grow * p.ldo + gcol] = fmaxf(v, 0.f);
   } else if constexpr (EPI == DEC_RESADD) {
-    p.out[(size_t)grow * p.ldo + gcol] = p.resid[(size_t)grow * p.ldo + gcol] + v;
+    const float r = RLN ? rn[row][gcol] : p.resid[(size_t)grow * p.ldo + gcol];
+    p.out[(size_t)grow * p.ldo + gcol] = r + v;
   } else if constexpr (EPI == DEC_QKV) {
-    const int t = p.st->t;
     if (gcol < p.d) {
       p.out[(size_t)grow * p.d + gcol] = v;
     } else if (gcol < 2 * p.d) {
@@ -79,179 +162,165 @@ __global__ void __launch_bounds__(256) rowgemm_kernel(RowGemmParams p) {
       p.vcache[((size_t)grow * p.max_pos + t) * p.d + (gcol - 2 * p.d)] = v;
     }
   } else {  // DEC_LOGITS
-    float* slot = p.out + (p.hist_stride ? (size_t)p.st->t * p.hist_stride : 0);
+    float* slot = p.out + (p.hist_stride ? (size_t)t * p.hist_stride : 0);
     slot[(size_t)grow * p.ldo + gcol] = v;
   }
 }
 
-template <int EPI>
+template <int EPI, bool ALN, bool RLN>
 void launch_rowgemm_k(const RowGemmParams& p, dim3 grid, hipStream_t s) {
   if (p.K == 256) {
-    rowgemm_kernel<EPI, 64><<<grid, 256, 0, s>>>(p);
+    rowgemm_kernel<EPI, 64, ALN, RLN><<<grid, 256, 0, s>>>(p);
   } else if (p.K == 512) {
-    rowgemm_kernel<EPI, 128><<<grid, 256, 0, s>>>(p);
+    rowgemm_kernel<EPI, 128, ALN, RLN><<<grid, 256, 0, s>>>(p);
   } else {
     throw std::runtime_error("rowgemm: K must be 256 or 512");
   }
 }
 
-// ------------------------------------------------------------------ embedding
-// x[b] = embedding[feed[b][t]] + pos_encoder[t]   (src/model_swin.py:73-75).
-// Single workgroup: it advances DecodeState.t before any other kernel of the step.
-__global__ void __launch_bounds__(256) dec_embed_kernel(DecodeState* st, const int32_t* __restrict__ feed, int ld_ids,
-                                                        const float* __restrict__ emb, const float* __restrict__ pos,
-                                                        float* __restrict__ x, int B, int d) {
-  __shared__ int s_t;
-  if (threadIdx.x == 0) {
-    int t = -1;
-    if (!st->done) {
-      t = st->t + 1;
-      if (t >= st->max_steps) {
-        st->done = 1;
-        st->nsteps = st->max_steps;
-        t = -1;
-      } else {
-        st->t = t;
-      }
-    }
-    s_t = t;
-  }
-  __syncthreads();
-  const int t = s_t;
-  if (t < 0) return;
-  for (int idx = threadIdx.x; idx < B * d; idx += blockDim.x) {
-    const int b = idx / d;
-    const int c = idx - b * d;
-    const int tok = feed[(size_t)b * ld_ids + t];
-    x[idx] = emb[(size_t)tok * d + c] + pos[(size_t)t * d + c];
+template <int EPI>
+void launch_rowgemm_e(const RowGemmParams& p, dim3 grid, hipStream_t s) {
+  const bool aln = p.a_ln_g != nullptr, rln = p.r_ln_g != nullptr;
+  if (aln && rln) throw std::runtime_error("rowgemm: LayerNorm on both A and resid is not built");
+  if (aln && p.K != kD) throw std::runtime_error("rowgemm: LayerNorm prologue needs K == d_model");
+  if (aln) {
+    launch_rowgemm_k<EPI, true, false>(p, grid, s);
+  } else if (rln) {
+    launch_rowgemm_k<EPI, false, true>(p, grid, s);
+  } else {
+    launch_rowgemm_k<EPI, false, false>(p, grid, s);
   }
 }
 
-// ------------------------------------------------------------------ LayerNorm(d)
-__global__ void __launch_bounds__(256) dec_layernorm_kernel(const DecodeState* st, const float* __restrict__ y,
-                                                            const float* __restrict__ g,
-                                                            const float* __restrict__ bta, float* __restrict__ x,
-                                                            int B, int d) {
-  if (st->done) return;
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= B) return;
-  const float* src = y + (size_t)row * d;
-  float v[4];
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = lane + 64 * i;
-    v[i] = c < d ? src[c] : 0.f;
-    s += v[i];
-  }
-  const float mean = wave_sum(s) / (float)d;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = lane + 64 * i;
-    if (c < d) {
-      const float t = v[i] - mean;
-      q += t * t;
-    }
-  }
-  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)d + 1e-5f);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = lane + 64 * i;
-    if (c < d) x[(size_t)row * d + c] = (v[i] - mean) * rstd * g[c] + bta[c];
-  }
+// ------------------------------------------------------------------ embedding of step 0
+// x[b] = embedding[feed[b][0]] + pos_encoder[0]   (src/model_swin.py:73-75).
+__global__ void __launch_bounds__(256) dec_embed0_kernel(const int32_t* __restrict__ feed, int ld_ids,
+                                                         const float* __restrict__ emb, const float* __restrict__ pos,
+                                                         float* __restrict__ x, int d) {
+  const int b = blockIdx.x;
+  const int tok = feed[(size_t)b * ld_ids];
+  for (int c = threadIdx.x; c < d; c += blockDim.x) x[(size_t)b * d + c] = emb[(size_t)tok * d + c] + pos[c];
 }
 
 // ------------------------------------------------------------------ attention
-// One wave per (row b, head h).  Scores q·k * 1/sqrt(32) for n keys, softmax with a
-// wave max/sum reduce, output Σ_j e_j v_j / Σ_j e_j (normalised at the end, like the
-// CPU flash-attention SDPA kernel the reference's F.multi_head_attention_forward
-// reaches).  Lane j scores keys j, j+64, ...; for P·V the two half-waves take even
-// and odd keys with lane&31 as the head-dim index (coalesced 128-B rows).
-__device__ __forceinline__ void attend(const float* __restrict__ qrow, const float* __restrict__ kbase,
-                                       const float* __restrict__ vbase, size_t kv_stride, int n,
-                                       float* __restrict__ out, float* p) {
-  const int lane = threadIdx.x & 63;
-  float qv[kHeadDim];
+// Newest position of row b against n keys, HB heads per workgroup (4 waves).  A key
+// row slice of HB*32 floats is read by 8*HB lanes (one float4 each), so one wave
+// instruction covers 64/(8*HB) keys with full 128-B head rows; scores q·k·1/sqrt(32)
+// are reduced over the 8 lanes of a head.  Softmax is exp(s - max) with the sum
+// applied at the end (Σ e v / Σ e), as in the CPU flash-attention SDPA kernel the
+// reference's F.multi_head_attention_forward reaches.
+template <int HB, int NIT>
+__global__ void __launch_bounds__(256) dec_attn_kernel(const DecodeState* st, int t, const float* __restrict__ q,
+                                                       const float* __restrict__ K, const float* __restrict__ V,
+                                                       size_t kv_b_stride, int kv_row_stride, int n_fixed,
+                                                       float* __restrict__ out, int d) {
+  constexpr int DIMS = 32 * HB;
+  constexpr int LPR = DIMS / 4;  // lanes per key row
+  constexpr int RPW = 64 / LPR;  // key rows per wave instruction
+  constexpr int MAXN = NIT * 4 * RPW;  // key rows per lane: NIT (upper bound)
+  __shared__ float S[HB][MAXN];
+  __shared__ float ssum[HB];
+  __shared__ floatx4 red[4][RPW][LPR];
+
+  const int n = n_fixed ? n_fixed : t + 1;
+  const int b = blockIdx.x;
+  const int hg = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int rsub = lane / LPR;
+  const int li = lane % LPR;
+  const int c4 = li * 4;
+  const int hl = c4 / 32;
+
+  const floatx4 q4 = *reinterpret_cast<const floatx4*>(q + (size_t)b * d + hg * DIMS + c4);
+  const float* Kb = K + (size_t)b * kv_b_stride + hg * DIMS + c4;
+  const float* Vb = V + (size_t)b * kv_b_stride + hg * DIMS + c4;
+  const int m_first = wave * RPW + rsub;
+  const int niter = (n + 4 * RPW - 1) / (4 * RPW);
+
+  // issue every K and V row load of this lane before using any of them
+  floatx4 kk[NIT], vv[NIT];
 #pragma unroll
-  for (int i = 0; i < kHeadDim / 4; ++i) {
-    const floatx4 t = *reinterpret_cast<const floatx4*>(qrow + 4 * i);
-    qv[4 * i] = t[0];
-    qv[4 * i + 1] = t[1];
-    qv[4 * i + 2] = t[2];
-    qv[4 * i + 3] = t[3];
-  }
-  float m = -INFINITY;
-  for (int j = lane; j < n; j += 64) {
-    const float* kr = kbase + (size_t)j * kv_stride;
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < kHeadDim / 4; ++i) {
-      const floatx4 kk = *reinterpret_cast<const floatx4*>(kr + 4 * i);
-      s = fmaf(qv[4 * i], kk[0], s);
-      s = fmaf(qv[4 * i + 1], kk[1], s);
-      s = fmaf(qv[4 * i + 2], kk[2], s);
-      s = fmaf(qv[4 * i + 3], kk[3], s);
+  for (int it = 0; it < NIT; ++it) {
+    const int m = m_first + it * 4 * RPW;
+    if (it < niter && m < n) {
+      kk[it] = *reinterpret_cast<const floatx4*>(Kb + (size_t)m * kv_row_stride);
+      vv[it] = *reinterpret_cast<const floatx4*>(Vb + (size_t)m * kv_row_stride);
+    } else {
+      kk[it] = floatx4{0.f, 0.f, 0.f, 0.f};
+      vv[it] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
-    s *= kAttnScale;
-    p[j] = s;
-    m = fmaxf(m, s);
   }
-  m = wave_max(m);
-  float sum = 0.f;
-  for (int j = lane; j < n; j += 64) {
-    const float e = expf(p[j] - m);
-    p[j] = e;
-    sum += e;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int m = m_first + it * 4 * RPW;
+    float s = q4[0] * kk[it][0];
+    s = fmaf(q4[1], kk[it][1], s);
+    s = fmaf(q4[2], kk[it][2], s);
+    s = fmaf(q4[3], kk[it][3], s);
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    if ((li & 7) == 0 && it < niter && m < n) S[hl][m] = s * kAttnScale;
   }
-  sum = wave_sum(sum);
   __syncthreads();
-  const int dd = lane & 31;
-  const int half = lane >> 5;
-  float o = 0.f;
-  for (int j = half; j < n; j += 2) o = fmaf(p[j], vbase[(size_t)j * kv_stride + dd], o);
-  o += __shfl_xor(o, 32, 64);
-  if (half == 0) out[dd] = o / sum;
-}
 
-__global__ void __launch_bounds__(64) dec_self_attn_kernel(const DecodeState* st, const float* __restrict__ q,
-                                                           const float* __restrict__ kc,
-                                                           const float* __restrict__ vc, float* __restrict__ out,
-                                                           int d, int max_pos) {
-  if (st->done) return;
-  __shared__ float p[256];
-  const int b = blockIdx.x;
-  const int h = blockIdx.y;
-  const int n = st->t + 1;
-  const size_t base = (size_t)b * max_pos * d + h * kHeadDim;
-  attend(q + (size_t)b * d + h * kHeadDim, kc + base, vc + base, d, n, out + (size_t)b * d + h * kHeadDim, p);
-}
+  for (int h = wave; h < HB; h += 4) {
+    float mx = -INFINITY;
+    for (int j = lane; j < n; j += 64) mx = fmaxf(mx, S[h][j]);
+    mx = wave_max(mx);
+    float sum = 0.f;
+    for (int j = lane; j < n; j += 64) {
+      const float e = expf(S[h][j] - mx);
+      S[h][j] = e;
+      sum += e;
+    }
+    sum = wave_sum(sum);
+    if (lane == 0) ssum[h] = sum;
+  }
+  __syncthreads();
 
-__global__ void __launch_bounds__(64) dec_cross_attn_kernel(const DecodeState* st, const float* __restrict__ q,
-                                                            const float* __restrict__ memkv, int ld_kv, int koff,
-                                                            int voff, float* __restrict__ out, int M, int d) {
-  if (st->done) return;
-  __shared__ float p[1024];
-  const int b = blockIdx.x;
-  const int h = blockIdx.y;
-  const size_t base = (size_t)b * M * ld_kv + h * kHeadDim;
-  attend(q + (size_t)b * d + h * kHeadDim, memkv + base + koff, memkv + base + voff, ld_kv, M,
-         out + (size_t)b * d + h * kHeadDim, p);
+  floatx4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int m = m_first + it * 4 * RPW;
+    if (it < niter && m < n) {
+      const float pm = S[hl][m];
+      o[0] = fmaf(pm, vv[it][0], o[0]);
+      o[1] = fmaf(pm, vv[it][1], o[1]);
+      o[2] = fmaf(pm, vv[it][2], o[2]);
+      o[3] = fmaf(pm, vv[it][3], o[3]);
+    }
+  }
+  red[wave][rsub][li] = o;
+  __syncthreads();
+  if (tid < DIMS && !dec_skip(st, t)) {
+    const int l4 = tid / 4;
+    const int e = tid % 4;
+    float acc = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) acc += red[w][r][l4][e];
+    out[(size_t)b * d + hg * DIMS + tid] = acc / ssum[tid / 32];
+  }
 }
 
 // ------------------------------------------------------------------ greedy select
 // argmax over the vocabulary (first maximal index, as torch.argmax), log-prob of the
 // chosen token log(softmax + 1e-10) (app/src/im2latex.py:33-39), EOS bookkeeping for
-// the batch-global stop (src/inference.py:23-25).
-__global__ void __launch_bounds__(256) dec_argmax_kernel(DecodeState* st, const float* __restrict__ logits,
-                                                         size_t hist_stride, int ldl, int V, int B,
+// the batch-global stop (src/inference.py:23-25), and the embedding of the token fed
+// to step t+1.
+__global__ void __launch_bounds__(256) dec_argmax_kernel(DecodeState* st, int t, int last_step,
+                                                         const float* __restrict__ logits, size_t hist_stride, int ldl,
+                                                         int V,
                                                          int32_t* __restrict__ ids, int32_t* __restrict__ feed,
                                                          const int32_t* __restrict__ forced, int ld_ids,
                                                          float* __restrict__ logp, int32_t* __restrict__ finished,
-                                                         int eos) {
-  if (st->done) return;
-  const int t = st->t;
+                                                         int eos, int stop_batch, const float* __restrict__ emb,
+                                                         const float* __restrict__ pos, float* __restrict__ x,
+                                                         int d) {
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -276,20 +345,21 @@ __global__ void __launch_bounds__(256) dec_argmax_kernel(DecodeState* st, const 
     }
   }
   __shared__ float sv[4];
-  __shared__ int si[4];
+  __shared__ int si_[4];
   __shared__ float ss[4];
+  __shared__ int s_next;
   if (lane == 0) {
     sv[wave] = best;
-    si[wave] = bidx;
+    si_[wave] = bidx;
   }
   __syncthreads();
   best = sv[0];
-  bidx = si[0];
+  bidx = si_[0];
 #pragma unroll
   for (int w = 1; w < 4; ++w) {
-    if (sv[w] > best || (sv[w] == best && si[w] < bidx)) {
+    if (sv[w] > best || (sv[w] == best && si_[w] < bidx)) {
       best = sv[w];
-      bidx = si[w];
+      bidx = si_[w];
     }
   }
   float sum = 0.f;
@@ -297,20 +367,29 @@ __global__ void __launch_bounds__(256) dec_argmax_kernel(DecodeState* st, const 
   sum = wave_sum(sum);
   if (lane == 0) ss[wave] = sum;
   __syncthreads();
-  if (tid != 0) return;
-  sum = ((ss[0] + ss[1]) + ss[2]) + ss[3];
-  const int S1 = ld_ids;
-  ids[(size_t)b * S1 + t + 1] = bidx;
-  feed[(size_t)b * S1 + t + 1] = forced ? forced[(size_t)b * S1 + t + 1] : bidx;
-  if (logp) logp[(size_t)b * (S1 - 1) + t] = logf(1.0f / sum + 1e-10f);
-  if (bidx == eos && !finished[b]) {
-    finished[b] = 1;
-    const int before = atomicAdd(&st->nfinished, 1);
-    if (before == B - 1 && st->stop_mode == 0) {
-      st->nsteps = t + 1;
+  if (dec_skip(stop_batch ? st : nullptr, t)) return;
+  if (tid == 0) {
+    sum = ((ss[0] + ss[1]) + ss[2]) + ss[3];
+    const int next = forced ? forced[(size_t)b * ld_ids + t + 1] : bidx;
+    ids[(size_t)b * ld_ids + t + 1] = bidx;
+    feed[(size_t)b * ld_ids + t + 1] = next;
+    logp[(size_t)b * (ld_ids - 1) + t] = logf(1.0f / sum + 1e-10f);
+    s_next = next;
+    if (bidx == eos && !finished[b]) {
+      finished[b] = 1;
+      atomicMax(&st->last_finish, t);
       __threadfence();
-      st->done = 1;
+      const int before = atomicAdd(&st->nfinished, 1);
+      if (before == st->batch - 1 && stop_batch) {
+        __threadfence();
+        st->done_step = atomicMax(&st->last_finish, t);
+      }
     }
+  }
+  __syncthreads();
+  if (!last_step) {
+    const int tok = s_next;
+    for (int c = tid; c < d; c += 256) x[(size_t)b * d + c] = emb[(size_t)tok * d + c] + pos[(size_t)(t + 1) * d + c];
   }
 }
 
@@ -318,50 +397,50 @@ __global__ void __launch_bounds__(256) dec_argmax_kernel(DecodeState* st, const 
 
 void launch_rowgemm(const RowGemmParams& p, hipStream_t s) {
   if (p.N % 16 != 0) throw std::runtime_error("rowgemm: N must be padded to 16");
+  if (p.d != kD) throw std::runtime_error("rowgemm: d_model must be 256");
   dim3 grid(p.N / 16, (p.B + 15) / 16);
   switch (p.epi) {
-    case DEC_STORE: launch_rowgemm_k<DEC_STORE>(p, grid, s); break;
-    case DEC_RELU: launch_rowgemm_k<DEC_RELU>(p, grid, s); break;
-    case DEC_RESADD: launch_rowgemm_k<DEC_RESADD>(p, grid, s); break;
-    case DEC_QKV: launch_rowgemm_k<DEC_QKV>(p, grid, s); break;
-    case DEC_LOGITS: launch_rowgemm_k<DEC_LOGITS>(p, grid, s); break;
+    case DEC_STORE: launch_rowgemm_e<DEC_STORE>(p, grid, s); break;
+    case DEC_RELU: launch_rowgemm_e<DEC_RELU>(p, grid, s); break;
+    case DEC_RESADD: launch_rowgemm_e<DEC_RESADD>(p, grid, s); break;
+    case DEC_QKV: launch_rowgemm_e<DEC_QKV>(p, grid, s); break;
+    case DEC_LOGITS: launch_rowgemm_e<DEC_LOGITS>(p, grid, s); break;
     default: throw std::runtime_error("rowgemm: bad epilogue");
   }
   MOCR_HIP_CHECK(hipGetLastError());
 }
 
-void launch_dec_embed(DecodeState* st, const int32_t* feed, int ld_ids, const float* emb, const float* pos, float* x,
-                      int B, int d, hipStream_t s) {
-  dec_embed_kernel<<<1, 256, 0, s>>>(st, feed, ld_ids, emb, pos, x, B, d);
-  MOCR_HIP_CHECK(hipGetLastError());
-}
-
-void launch_dec_layernorm(const DecodeState* st, const float* y, const float* g, const float* b, float* x, int B,
-                          int d, hipStream_t s) {
-  if (d > 256) throw std::runtime_error("dec_layernorm: d_model > 256");
-  dec_layernorm_kernel<<<(B + 3) / 4, 256, 0, s>>>(st, y, g, b, x, B, d);
-  MOCR_HIP_CHECK(hipGetLastError());
-}
-
-void launch_dec_self_attn(const DecodeState* st, const float* q, const float* kc, const float* vc, float* out, int B,
-                          int d, int heads, int max_pos, hipStream_t s) {
-  if (max_pos > 256) throw std::runtime_error("dec_self_attn: max_pos > 256");
-  dec_self_attn_kernel<<<dim3(B, heads), 64, 0, s>>>(st, q, kc, vc, out, d, max_pos);
-  MOCR_HIP_CHECK(hipGetLastError());
-}
-
-void launch_dec_cross_attn(const DecodeState* st, const float* q, const float* memkv, int ld_kv, int koff, int voff,
-                           float* out, int B, int M, int d, int heads, hipStream_t s) {
-  if (M > 1024) throw std::runtime_error("dec_cross_attn: more than 1024 memory tokens");
-  dec_cross_attn_kernel<<<dim3(B, heads), 64, 0, s>>>(st, q, memkv, ld_kv, koff, voff, out, M, d);
-  MOCR_HIP_CHECK(hipGetLastError());
-}
-
-void launch_dec_argmax(DecodeState* st, const float* logits, size_t hist_stride, int ldl, int V, int B, int32_t* ids,
-                       int32_t* feed, const int32_t* forced, int ld_ids, float* logp, int32_t* finished, int eos,
+void launch_dec_embed0(const int32_t* feed, int ld_ids, const float* emb, const float* pos, float* x, int B, int d,
                        hipStream_t s) {
-  dec_argmax_kernel<<<B, 256, 0, s>>>(st, logits, hist_stride, ldl, V, B, ids, feed, forced, ld_ids, logp, finished,
-                                      eos);
+  dec_embed0_kernel<<<B, 256, 0, s>>>(feed, ld_ids, emb, pos, x, d);
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_dec_attn(const DecodeState* st, int t, const float* q, const float* K, const float* V,
+                     size_t kv_b_stride, int kv_row_stride, int n_fixed, int n_max, float* out, int B, int d,
+                     int heads, hipStream_t s) {
+  constexpr int HB = 2;
+  if (d != kD || heads * 32 != d) throw std::runtime_error("dec_attn: d_model 256 with 8 heads of 32");
+  if (n_max > 256) throw std::runtime_error("dec_attn: at most 256 keys");
+  const int nit = (n_max + 15) / 16;  // 16 key rows per workgroup pass (4 waves x 4 rows)
+  const dim3 grid(B, heads / HB);
+#define MOCR_ATTN(N) dec_attn_kernel<HB, N><<<grid, 256, 0, s>>>(st, t, q, K, V, kv_b_stride, kv_row_stride, n_fixed, out, d)
+  if (nit <= 2) MOCR_ATTN(2);
+  else if (nit <= 4) MOCR_ATTN(4);
+  else if (nit <= 8) MOCR_ATTN(8);
+  else if (nit <= 10) MOCR_ATTN(10);
+  else if (nit <= 12) MOCR_ATTN(12);
+  else MOCR_ATTN(16);
+#undef MOCR_ATTN
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_dec_argmax(DecodeState* st, int t, int last_step, const float* logits, size_t hist_stride, int ldl,
+                       int V, int B, int32_t* ids, int32_t* feed, const int32_t* forced, int ld_ids, float* logp,
+                       int32_t* finished, int eos, int stop_batch, const float* emb, const float* pos, float* x,
+                       int d, hipStream_t s) {
+  dec_argmax_kernel<<<B, 256, 0, s>>>(st, t, last_step, logits, hist_stride, ldl, V, ids, feed, forced, ld_ids, logp,
+                                      finished, eos, stop_batch, emb, pos, x, d);
   MOCR_HIP_CHECK(hipGetLastError());
 }
 

@@ -203,7 +203,8 @@ struct mocr_engine {
   int partial_stage = -1;
 
   // decoder state
-  float *dx = nullptr, *dq = nullptr, *datt = nullptr, *dy = nullptr, *dh = nullptr, *dlogits = nullptr;
+  float *dx = nullptr, *dq = nullptr, *datt = nullptr, *dh = nullptr, *dlogits = nullptr;
+  float *dy_sa = nullptr, *dy_ca = nullptr, *dy_ff = nullptr;
   float* dlogits_hist = nullptr;
   float *kcache = nullptr, *vcache = nullptr;
   int32_t *ids = nullptr, *feed = nullptr, *forced = nullptr, *finished = nullptr;
@@ -227,7 +228,7 @@ struct mocr_engine {
       (void)hipEventDestroy(r.e1);
     }
     void* bufs[] = {dw,      fcw_pad, fcb_pad, kvw_all, kvb_all, img,  X,        X2,       XW,     QKV,
-                    ATT,     HID,     MEM,     MEMKV,   dx,      dq,   datt,     dy,       dh,     dlogits,
+                    ATT,     HID,     MEM,     MEMKV,   dx,      dq,   datt,     dy_sa,    dy_ca,  dy_ff, dh, dlogits,
                     dlogits_hist, kcache, vcache, ids, feed, forced, finished, logp, st};
     for (void* p : bufs)
       if (p) (void)hipFree(p);
@@ -295,7 +296,9 @@ struct mocr_engine {
     dx = dalloc<float>(B * d);
     dq = dalloc<float>(B * d);
     datt = dalloc<float>(B * d);
-    dy = dalloc<float>(B * d);
+    dy_sa = dalloc<float>(B * d);
+    dy_ca = dalloc<float>(B * d);
+    dy_ff = dalloc<float>(B * d);
     dh = dalloc<float>(B * cfg.d_ff);
     dlogits = dalloc<float>(B * Vpad);
     kcache = dalloc<float>(L * B * cfg.max_pos * d);
@@ -404,7 +407,7 @@ struct mocr_engine {
 
   // ---------------------------------------------------------------- encoder
   void gemm(const char* name, const float* A, const float* Wt, const float* bias, float* C, int Mrows, int N, int K,
-            int epi, const WinGeom* wg, long alg_rows) {
+            int epi, const WinGeom* wg, long alg_rows, int col_split = 0, size_t split_stride = 0) {
     GemmParams p{};
     p.A = A;
     p.W = Wt;
@@ -418,6 +421,8 @@ struct mocr_engine {
     p.ldc = N;
     p.epi = epi;
     if (wg) p.win = *wg;
+    p.col_split = col_split;
+    p.split_stride = split_stride;
     const double flops = 2.0 * alg_rows * N * K;
     const double bytes = 4.0 * ((double)alg_rows * K + (double)N * K + (double)alg_rows * N *
                                                                             (epi == EPI_RESADD || epi == EPI_WINRES ? 2 : 1));
@@ -472,7 +477,7 @@ struct mocr_engine {
     }
     gemm("memproj", X, W(lay->projw), W(lay->projb), MEM, B * M, (int)d, kEncDim, EPI_STORE, nullptr, (long)B * M);
     gemm("crosskv", MEM, kvw_all, kvb_all, MEMKV, B * M, (int)(L * 2 * d), (int)d, EPI_STORE, nullptr,
-         (long)B * M);
+         (long)B * M, (int)(2 * d), (size_t)cfg.max_batch * M * 2 * d);
     MOCR_HIP_CHECK(hipStreamSynchronize(stream));
     if (timing) flush_timing();
     encoded = true;
@@ -493,50 +498,70 @@ struct mocr_engine {
   }
 
   // ---------------------------------------------------------------- decoder
-  void record_step(int B, bool hist, bool use_forced) {
+  // One greedy step t.  Buffers: dx = fed-token embedding (layer-0 input),
+  // ysa/yca/yff = pre-LayerNorm sums of the three post-norm sublayers; LN1/LN2/LN3 are
+  // applied by their consumers.  stp = stop state (nullptr unless batch-global stop).
+  void record_step(int B, int t, int max_steps, bool hist, bool use_forced, bool stop_batch) {
     const int d = cfg.d_model, L = cfg.n_layers;
     const size_t cache_layer = (size_t)cfg.max_batch * cfg.max_pos * d;
-    launch_dec_embed(st, feed, ld_ids, W(lay->emb), W(lay->pos), dx, B, d, stream);
-    for (int l = 0; l < L; ++l) {
-      const DecLayerW& w = lay->layers[l];
-      float* kc = kcache + l * cache_layer;
-      float* vc = vcache + l * cache_layer;
+    const size_t kv_layer = (size_t)cfg.max_batch * M * 2 * d;
+    const DecodeState* stp = stop_batch ? st : nullptr;
+    hipStream_t s = stream;
+    auto base = [&]() {
       RowGemmParams p{};
       p.B = B;
-      p.st = st;
+      p.st = stp;
+      p.t = t;
       p.d = d;
       p.max_pos = cfg.max_pos;
-      // self-attention block (post-norm): x = norm1(x + SA(x))
-      p.A = dx; p.W = W(w.sa_inw); p.bias = W(w.sa_inb); p.out = dq; p.kcache = kc; p.vcache = vc;
-      p.N = 3 * d; p.K = d; p.ldo = d; p.n_valid = 3 * d; p.epi = DEC_QKV;
-      launch_rowgemm(p, stream);
-      launch_dec_self_attn(st, dq, kc, vc, datt, B, d, cfg.n_heads, cfg.max_pos, stream);
-      p.A = datt; p.W = W(w.sa_ow); p.bias = W(w.sa_ob); p.out = dy; p.resid = dx;
-      p.N = d; p.n_valid = d; p.epi = DEC_RESADD;
-      launch_rowgemm(p, stream);
-      launch_dec_layernorm(st, dy, W(w.n1w), W(w.n1b), dx, B, d, stream);
-      // cross-attention block: x = norm2(x + MHA(x, mem))
-      p.A = dx; p.W = W(w.ca_inw); p.bias = W(w.ca_inb); p.out = dq; p.resid = nullptr;
-      p.N = d; p.n_valid = d; p.epi = DEC_STORE;
-      launch_rowgemm(p, stream);
-      launch_dec_cross_attn(st, dq, MEMKV, L * 2 * d, l * 2 * d, l * 2 * d + d, datt, B, M, d, cfg.n_heads, stream);
-      p.A = datt; p.W = W(w.ca_ow); p.bias = W(w.ca_ob); p.out = dy; p.resid = dx;
-      p.N = d; p.n_valid = d; p.epi = DEC_RESADD;
-      launch_rowgemm(p, stream);
-      launch_dec_layernorm(st, dy, W(w.n2w), W(w.n2b), dx, B, d, stream);
-      // feed-forward block: x = norm3(x + W2 relu(W1 x))
-      p.A = dx; p.W = W(w.l1w); p.bias = W(w.l1b); p.out = dh; p.resid = nullptr;
+      return p;
+    };
+    for (int l = 0; l < L; ++l) {
+      const DecLayerW& w = lay->layers[l];
+      const DecLayerW* prev = l ? &lay->layers[l - 1] : nullptr;
+      float* kc = kcache + l * cache_layer;
+      float* vc = vcache + l * cache_layer;
+      // layer input: embedding (l = 0) or LN3 of the previous layer
+      const float* xin = l ? dy_ff : dx;
+      const float* xin_g = l ? W(prev->n3w) : nullptr;
+      const float* xin_b = l ? W(prev->n3b) : nullptr;
+      // self-attention block: y_sa = x + SA(x)
+      RowGemmParams p = base();
+      p.A = xin; p.a_ln_g = xin_g; p.a_ln_b = xin_b; p.W = W(w.sa_inw); p.bias = W(w.sa_inb);
+      p.out = dq; p.kcache = kc; p.vcache = vc; p.N = 3 * d; p.K = d; p.ldo = d; p.n_valid = 3 * d;
+      p.epi = DEC_QKV;
+      launch_rowgemm(p, s);
+      launch_dec_attn(stp, t, dq, kc, vc, (size_t)cfg.max_pos * d, d, t + 1, t + 1, datt, B, d, cfg.n_heads, s);
+      p = base();
+      p.A = datt; p.W = W(w.sa_ow); p.bias = W(w.sa_ob); p.out = dy_sa; p.resid = xin; p.r_ln_g = xin_g;
+      p.r_ln_b = xin_b; p.N = d; p.K = d; p.ldo = d; p.n_valid = d; p.epi = DEC_RESADD;
+      launch_rowgemm(p, s);
+      // cross-attention block: y_ca = LN1(y_sa) + MHA(LN1(y_sa), mem)
+      p = base();
+      p.A = dy_sa; p.a_ln_g = W(w.n1w); p.a_ln_b = W(w.n1b); p.W = W(w.ca_inw); p.bias = W(w.ca_inb);
+      p.out = dq; p.N = d; p.K = d; p.ldo = d; p.n_valid = d; p.epi = DEC_STORE;
+      launch_rowgemm(p, s);
+      const float* memk = MEMKV + l * kv_layer;
+      launch_dec_attn(stp, t, dq, memk, memk + d, (size_t)M * 2 * d, 2 * d, M, M, datt, B, d, cfg.n_heads, s);
+      p = base();
+      p.A = datt; p.W = W(w.ca_ow); p.bias = W(w.ca_ob); p.out = dy_ca; p.resid = dy_sa; p.r_ln_g = W(w.n1w);
+      p.r_ln_b = W(w.n1b); p.N = d; p.K = d; p.ldo = d; p.n_valid = d; p.epi = DEC_RESADD;
+      launch_rowgemm(p, s);
+      // feed-forward block: y_ff = LN2(y_ca) + W2 relu(W1 LN2(y_ca))
+      p = base();
+      p.A = dy_ca; p.a_ln_g = W(w.n2w); p.a_ln_b = W(w.n2b); p.W = W(w.l1w); p.bias = W(w.l1b); p.out = dh;
       p.N = cfg.d_ff; p.K = d; p.ldo = cfg.d_ff; p.n_valid = cfg.d_ff; p.epi = DEC_RELU;
-      launch_rowgemm(p, stream);
-      p.A = dh; p.W = W(w.l2w); p.bias = W(w.l2b); p.out = dy; p.resid = dx;
-      p.N = d; p.K = cfg.d_ff; p.ldo = d; p.n_valid = d; p.epi = DEC_RESADD;
-      launch_rowgemm(p, stream);
-      launch_dec_layernorm(st, dy, W(w.n3w), W(w.n3b), dx, B, d, stream);
+      launch_rowgemm(p, s);
+      p = base();
+      p.A = dh; p.W = W(w.l2w); p.bias = W(w.l2b); p.out = dy_ff; p.resid = dy_ca; p.r_ln_g = W(w.n2w);
+      p.r_ln_b = W(w.n2b); p.N = d; p.K = cfg.d_ff; p.ldo = d; p.n_valid = d; p.epi = DEC_RESADD;
+      launch_rowgemm(p, s);
     }
-    RowGemmParams p{};
-    p.B = B;
-    p.st = st;
-    p.A = dx;
+    const DecLayerW& last = lay->layers[L - 1];
+    RowGemmParams p = base();
+    p.A = dy_ff;
+    p.a_ln_g = W(last.n3w);
+    p.a_ln_b = W(last.n3b);
     p.W = fcw_pad;
     p.bias = fcb_pad;
     p.out = hist ? dlogits_hist : dlogits;
@@ -546,19 +571,25 @@ struct mocr_engine {
     p.ldo = Vpad;
     p.n_valid = cfg.vocab;
     p.epi = DEC_LOGITS;
-    launch_rowgemm(p, stream);
-    launch_dec_argmax(st, p.out, p.hist_stride, Vpad, cfg.vocab, B, ids, feed, use_forced ? forced : nullptr, ld_ids,
-                      logp, finished, cfg.eos_id, stream);
+    launch_rowgemm(p, s);
+    launch_dec_argmax(st, t, t + 1 >= max_steps, p.out, p.hist_stride, Vpad, cfg.vocab, B, ids, feed,
+                      use_forced ? forced : nullptr, ld_ids, logp, finished, cfg.eos_id, stop_batch ? 1 : 0,
+                      W(lay->emb), W(lay->pos), dx, d, s);
   }
 
-  hipGraphExec_t graph_for(int B, bool hist, bool use_forced) {
-    auto key = std::make_tuple(B, (int)hist, (int)use_forced);
+  // Graph of steps [c*kDecodeChunk, min(max_steps, (c+1)*kDecodeChunk)), step indices baked in.
+  hipGraphExec_t graph_for(int B, int c, int max_steps, bool hist, bool use_forced, bool stop_batch) {
+    const int t0 = c * kDecodeChunk;
+    const int t1 = std::min(max_steps, t0 + kDecodeChunk);
+    const bool ends = t1 == max_steps;  // the last step skips the next embedding
+    const int flags = (int)hist | (int)use_forced << 1 | (int)stop_batch << 2 | (int)ends << 3;
+    auto key = std::make_tuple(B, t0 * 1000 + t1, flags);
     auto it = graphs.find(key);
     if (it != graphs.end()) return it->second;
     hipGraph_t g;
     MOCR_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     try {
-      for (int i = 0; i < kDecodeChunk; ++i) record_step(B, hist, use_forced);
+      for (int t = t0; t < t1; ++t) record_step(B, t, max_steps, hist, use_forced, stop_batch);
     } catch (...) {
       (void)hipStreamEndCapture(stream, &g);
       throw;
@@ -578,6 +609,7 @@ struct mocr_engine {
     if (stop_mode != MOCR_STOP_BATCH && stop_mode != MOCR_STOP_NONE) throw std::runtime_error("bad stop_mode");
     MOCR_HIP_CHECK(hipSetDevice(device));
     const int B = cur_batch;
+    const bool stop_batch = stop_mode == MOCR_STOP_BATCH;
     if (want_logits && !dlogits_hist) dlogits_hist = dalloc<float>((size_t)cfg.max_pos * cfg.max_batch * Vpad);
     // ids/feed: column 0 = sos, the rest pad (src/inference.py:15)
     std::vector<int32_t> init((size_t)B * ld_ids, cfg.pad_id);
@@ -596,24 +628,24 @@ struct mocr_engine {
     }
     MOCR_HIP_CHECK(hipMemsetAsync(finished, 0, (size_t)B * 4, stream));
     DecodeState h{};
-    h.t = -1;
-    h.max_steps = max_steps;
-    h.stop_mode = stop_mode;
+    h.done_step = 0x7fffffff;
+    h.batch = B;
     MOCR_HIP_CHECK(hipMemcpyAsync(st, &h, sizeof(h), hipMemcpyHostToDevice, stream));
-    hipGraphExec_t exec = graph_for(B, want_logits, forced_host != nullptr);
+    launch_dec_embed0(feed, ld_ids, W(lay->emb), W(lay->pos), dx, B, cfg.d_model, stream);
     const int chunks = (max_steps + kDecodeChunk - 1) / kDecodeChunk;
     DecodeState hs{};
     for (int c = 0; c < chunks; ++c) {
-      MOCR_HIP_CHECK(hipGraphLaunch(exec, stream));
-      if (stop_mode == MOCR_STOP_BATCH && c + 1 < chunks) {
+      MOCR_HIP_CHECK(hipGraphLaunch(graph_for(B, c, max_steps, want_logits, forced_host != nullptr, stop_batch),
+                                    stream));
+      if (stop_batch && c + 1 < chunks) {
         MOCR_HIP_CHECK(hipMemcpyAsync(&hs, st, sizeof(hs), hipMemcpyDeviceToHost, stream));
         MOCR_HIP_CHECK(hipStreamSynchronize(stream));
-        if (hs.done) break;
+        if (hs.done_step != 0x7fffffff) break;
       }
     }
     MOCR_HIP_CHECK(hipMemcpyAsync(&hs, st, sizeof(hs), hipMemcpyDeviceToHost, stream));
     MOCR_HIP_CHECK(hipStreamSynchronize(stream));
-    return hs.done && hs.nsteps > 0 ? hs.nsteps : max_steps;
+    return stop_batch && hs.done_step != 0x7fffffff ? hs.done_step + 1 : max_steps;
   }
 
   void copy_ids(int32_t* dst, int max_steps, hipMemcpyKind kind) {

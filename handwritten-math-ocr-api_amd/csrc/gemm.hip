@@ -28,7 +28,12 @@ template <int EPI>
 __device__ __forceinline__ void epi_store(const GemmParams& p, int row, int col, float v) {
   if (p.bias) v += p.bias[col];
   if constexpr (EPI == EPI_STORE) {
-    p.C[(size_t)row * p.ldc + col] = v;
+    if (p.col_split) {
+      const int blk = col / p.col_split;
+      p.C[blk * p.split_stride + (size_t)row * p.col_split + (col - blk * p.col_split)] = v;
+    } else {
+      p.C[(size_t)row * p.ldc + col] = v;
+    }
   } else if constexpr (EPI == EPI_GELU) {
     p.C[(size_t)row * p.ldc + col] = gelu_erf(v);
   } else if constexpr (EPI == EPI_RESADD) {

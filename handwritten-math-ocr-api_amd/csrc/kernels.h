@@ -36,6 +36,8 @@ struct GemmParams {
   int lda, ldw, ldc;
   int epi;
   WinGeom win;
+  int col_split;       // EPI_STORE: column block width of a split layout (0 = plain [M, ldc])
+  size_t split_stride; // floats between column blocks: C[col/cs][row][col%cs]
 };
 
 void launch_gemm_f32(const GemmParams& p, hipStream_t s);
@@ -65,6 +67,8 @@ void launch_merge_ln(const float* X, const float* g, const float* b, float* Y, u
 void launch_f32_to_bf16(const float* x, uint16_t* y, size_t n, hipStream_t s);
 
 // ------------------------------------------------------------------ decoder
+// Every decode kernel takes its step index t as an argument (one captured graph per
+// chunk of steps) and `st` (nullable) for the batch-global stop.
 enum DecEpi : int {
   DEC_STORE = 0,   // out = acc + bias
   DEC_RELU = 1,    // out = relu(acc + bias)
@@ -74,11 +78,13 @@ enum DecEpi : int {
 };
 
 struct RowGemmParams {
-  const float* A;      // [B, K]
+  const float* A;      // [B, K]  (pre-LayerNorm sums when a_ln_g is set)
   const float* W;      // [N, K]
   const float* bias;   // [N]
   float* out;          // [B, ldo]
-  const float* resid;  // DEC_RESADD
+  const float* resid;  // DEC_RESADD: [B, ldo] (pre-LayerNorm sums when r_ln_g is set)
+  const float* a_ln_g; const float* a_ln_b;  // A := LayerNorm(A) * g + b, fused prologue
+  const float* r_ln_g; const float* r_ln_b;  // resid := LayerNorm(resid) * g + b
   float* kcache;       // DEC_QKV: [B, max_pos, d] for this layer
   float* vcache;
   int B, N, K, ldo;
@@ -86,27 +92,25 @@ struct RowGemmParams {
   int n_valid;         // columns < n_valid are real (fc_out padding)
   size_t hist_stride;  // DEC_LOGITS: floats between step slots (0: single slot)
   int epi;
+  int t;               // decode step
   const DecodeState* st;
 };
 void launch_rowgemm(const RowGemmParams& p, hipStream_t s);
 
-// Embedding of step t (single block; advances the step counter).
-void launch_dec_embed(DecodeState* st, const int32_t* feed, int ld_ids, const float* emb, const float* pos,
-                      float* x, int B, int d, hipStream_t s);
+// x[b] = embedding[feed[b][0]] + pos[0] and DecodeState init (outside the graph).
+void launch_dec_embed0(const int32_t* feed, int ld_ids, const float* emb, const float* pos, float* x, int B, int d,
+                       hipStream_t s);
 
-// Decoder LayerNorm over d (one wave per row).
-void launch_dec_layernorm(const DecodeState* st, const float* y, const float* g, const float* b, float* x, int B,
-                          int d, hipStream_t s);
+// Attention of the newest position over n keys (self: n = t+1 from the KV cache;
+// cross: n = M memory tokens).  K/V rows for image b start at K + b*kv_b_stride.
+void launch_dec_attn(const DecodeState* st, int t, const float* q, const float* K, const float* V,
+                     size_t kv_b_stride, int kv_row_stride, int n_fixed, int n_max, float* out, int B, int d,
+                     int heads, hipStream_t s);
 
-// Self-attention over the KV cache (keys 0..t) and cross-attention over memory K/V.
-void launch_dec_self_attn(const DecodeState* st, const float* q, const float* kc, const float* vc, float* out,
-                          int B, int d, int heads, int max_pos, hipStream_t s);
-void launch_dec_cross_attn(const DecodeState* st, const float* q, const float* memkv, int ld_kv, int koff,
-                           int voff, float* out, int B, int M, int d, int heads, hipStream_t s);
-
-// Argmax + log-prob + finish flags + next fed token.
-void launch_dec_argmax(DecodeState* st, const float* logits, size_t hist_stride, int ldl, int V, int B,
-                       int32_t* ids, int32_t* feed, const int32_t* forced, int ld_ids, float* logp,
-                       int32_t* finished, int eos, hipStream_t s);
+// Argmax + log-prob + finish flags + next fed token + next step's embedding.
+void launch_dec_argmax(DecodeState* st, int t, int last_step, const float* logits, size_t hist_stride, int ldl,
+                       int V, int B, int32_t* ids, int32_t* feed, const int32_t* forced, int ld_ids, float* logp,
+                       int32_t* finished, int eos, int stop_batch, const float* emb, const float* pos, float* x,
+                       int d, hipStream_t s);
 
 }  // namespace mocr

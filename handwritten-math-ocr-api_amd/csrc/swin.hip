@@ -179,82 +179,153 @@ __global__ void __launch_bounds__(256) merge_ln_kernel(const float* __restrict__
 }
 
 // ---------------------------------------------------------------- window attention
-// One workgroup per (window, head): Q/K/V 49x32 tiles staged in LDS, scores
-// (q*scale)·kᵀ + relative-position bias (+ -100 shift mask), row softmax with a
-// wave-wide max/sum reduce, then P·V.  q is scaled before the matmul and the mask is
-// added after the bias, as in torchvision.
-constexpr int QK_LD = kHeadDim + 1;
-constexpr int S_LD = kWinTok + 1;
+// One workgroup (4 waves) per (window, head) on v_mfma_f32_32x32x2_f32:
+//   S = (q * 32^-0.5) kᵀ  (49x49 padded to 64x64; wave w owns S block (w>>1, w&1)),
+//   + relative-position bias, + -100 where the shift-mask regions differ;
+//   row softmax through LDS (one wave per row, wave max/sum reduce);
+//   O = P V  (wave w owns row block w>>1 and key half w&1; the two halves are summed
+//   through LDS in a fixed order).
+// q/k fragments are read straight from the qkv rows (16 contiguous floats per lane:
+// lane half h feeds k = 16h + s at MFMA step s); V is staged transposed in LDS so the
+// P·V B-operand is also 16 contiguous floats per lane.  q is scaled before the matmul
+// and the mask added after the bias, as in torchvision.
+constexpr int SP = 68;  // padded LDS row stride (floats): 16-B aligned, 17 slots per row
 
 __global__ void __launch_bounds__(256) window_attention_kernel(const float* __restrict__ QKV,
                                                                const float* __restrict__ relbias,
                                                                float* __restrict__ O, uint16_t* __restrict__ O16,
                                                                int C, WinGeom wg) {
-  __shared__ float q[kWinTok * QK_LD];
-  __shared__ float k[kWinTok * QK_LD];
-  __shared__ float v[kWinTok * kHeadDim];
-  __shared__ float S[kWinTok * S_LD];
-  __shared__ int region[kWinTok];
+  __shared__ float S[64 * SP];
+  __shared__ float Vt[kHeadDim * SP];
+  __shared__ int region[64];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const long wg_idx = blockIdx.x;   // global window index (b * nWin + win)
+  const int l32 = lane & 31;
+  const int half = lane >> 5;
+  const long wg_idx = blockIdx.x;  // global window index (b * nWin + win)
   const int h = blockIdx.y;
   const int C3 = 3 * C;
   const size_t base = (size_t)wg_idx * kWinTok;
   const float scale = 0.17677669529663687f;  // 32 ** -0.5
 
-  for (int idx = tid; idx < kWinTok * kHeadDim; idx += 256) {
+  // V^T into LDS (zero for padded keys 49..63)
+  for (int idx = tid; idx < 64 * kHeadDim; idx += 256) {
     const int t = idx >> 5;
-    const int d = idx & 31;
-    const float* r = QKV + (base + t) * C3 + h * kHeadDim + d;
-    q[t * QK_LD + d] = r[0] * scale;
-    k[t * QK_LD + d] = r[C];
-    v[t * kHeadDim + d] = r[2 * C];
+    const int dd = idx & 31;
+    Vt[dd * SP + t] = t < kWinTok ? QKV[(base + t) * C3 + 2 * C + h * kHeadDim + dd] : 0.f;
   }
   const bool masked = (wg.sh + wg.sw) > 0;
   if (masked && tid < kWinTok) {
     const int win = (int)(wg_idx % wg.nWin);
     const int wy = win / wg.nWx;
     const int wx = win - wy * wg.nWx;
-    const int py = wy * kWin + tid / kWin;
-    const int px = wx * kWin + tid % kWin;
-    region[tid] = 3 * shift_region(py, wg.pH, wg.sh) + shift_region(px, wg.pW, wg.sw);
+    region[tid] = 3 * shift_region(wy * kWin + tid / kWin, wg.pH, wg.sh) +
+                  shift_region(wx * kWin + tid % kWin, wg.pW, wg.sw);
   }
-  __syncthreads();
 
-  const float* rb = relbias + (size_t)h * kWinTok * kWinTok;
-  for (int idx = tid; idx < kWinTok * kWinTok; idx += 256) {
-    const int i = idx / kWinTok;
-    const int j = idx - i * kWinTok;
-    float s = 0.f;
+  // ---- S block (bi, bj)
+  const int bi = wave >> 1, bj = wave & 1;
+  {
+    const int qi = bi * 32 + l32;
+    const int kj = bj * 32 + l32;
+    float qa[16], kb[16];
+    if (qi < kWinTok) {
+      const float* src = QKV + (base + qi) * C3 + h * kHeadDim + 16 * half;
 #pragma unroll
-    for (int d = 0; d < kHeadDim; ++d) s = fmaf(q[i * QK_LD + d], k[j * QK_LD + d], s);
-    s = s + rb[idx];
-    if (masked && region[i] != region[j]) s = s + (-100.0f);
-    S[i * S_LD + j] = s;
+      for (int i = 0; i < 4; ++i) {
+        const floatx4 v = *reinterpret_cast<const floatx4*>(src + 4 * i);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) qa[4 * i + e] = v[e] * scale;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) qa[i] = 0.f;
+    }
+    if (kj < kWinTok) {
+      const float* src = QKV + (base + kj) * C3 + C + h * kHeadDim + 16 * half;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const floatx4 v = *reinterpret_cast<const floatx4*>(src + 4 * i);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) kb[4 * i + e] = v[e];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) kb[i] = 0.f;
+    }
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[s], kb[s], acc, 0, 0, 0);
+    __syncthreads();  // region[] ready
+    const float* rb = relbias + (size_t)h * kWinTok * kWinTok;
+    const int col = bj * 32 + l32;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = bi * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+      if (row < kWinTok && col < kWinTok) {
+        float v = acc[r] + rb[row * kWinTok + col];
+        if (masked && region[row] != region[col]) v = v + (-100.0f);
+        S[row * SP + col] = v;
+      }
+    }
   }
   __syncthreads();
 
+  // ---- softmax over the 49 keys of each row; padded keys get P = 0
   for (int i = wave; i < kWinTok; i += 4) {
-    const float x = lane < kWinTok ? S[i * S_LD + lane] : -INFINITY;
+    const float x = lane < kWinTok ? S[i * SP + lane] : -INFINITY;
     const float m = wave_max(x);
     const float e = lane < kWinTok ? expf(x - m) : 0.f;
     const float sum = wave_sum(e);
-    if (lane < kWinTok) S[i * S_LD + lane] = e / sum;
+    S[i * SP + lane] = e / sum;  // lanes 49..63 write 0
   }
   __syncthreads();
 
-  for (int idx = tid; idx < kWinTok * kHeadDim; idx += 256) {
-    const int i = idx >> 5;
-    const int d = idx & 31;
-    float o = 0.f;
-#pragma unroll 7
-    for (int j = 0; j < kWinTok; ++j) o = fmaf(S[i * S_LD + j], v[j * kHeadDim + d], o);
-    const size_t off = (base + i) * C + h * kHeadDim + d;
-    if (O) O[off] = o;
-    if (O16) O16[off] = f32_to_bf16_rne(o);
+  // ---- O = P V: row block bi, key half kh
+  const int kh = wave & 1;
+  floatx16 o;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o[r] = 0.f;
+  {
+    const int pi = bi * 32 + l32;  // rows >= 49 read stale LDS rows: results discarded
+    const float* prow = &S[pi * SP + 32 * kh + 16 * half];
+    const float* vrow = &Vt[l32 * SP + 32 * kh + 16 * half];
+    float pa[16], vb[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const floatx4 p4 = *reinterpret_cast<const floatx4*>(prow + 4 * i);
+      const floatx4 v4 = *reinterpret_cast<const floatx4*>(vrow + 4 * i);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        pa[4 * i + e] = p4[e];
+        vb[4 * i + e] = v4[e];
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) o = __builtin_amdgcn_mfma_f32_32x32x2f32(pa[s], vb[s], o, 0, 0, 0);
+  }
+  __syncthreads();  // everyone is done reading S; reuse it for the key-half exchange
+  float* red = S;   // [2 row blocks][16 regs][64 lanes]
+  if (kh == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[(bi * 16 + r) * 64 + lane] = o[r];
+  }
+  __syncthreads();
+  if (kh == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = bi * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+      if (row < kWinTok) {
+        const float v = o[r] + red[(bi * 16 + r) * 64 + lane];
+        const size_t off = (base + row) * C + h * kHeadDim + l32;
+        if (O) O[off] = v;
+        if (O16) O16[off] = f32_to_bf16_rne(v);
+      }
+    }
   }
 }
 
