@@ -133,7 +133,9 @@ void check_config(const mocr_config& c) {
   req(c.n_layers >= 1 && c.n_layers <= 64, "n_layers");
   req(c.max_pos >= 2 && c.max_pos <= 256, "max_pos in [2,256]");
   req(c.max_batch >= 1 && c.max_batch <= 4096, "max_batch");
-  req(c.precision == MOCR_PRECISION_FP32 || c.precision == MOCR_PRECISION_BF16, "precision");
+  req(c.precision == MOCR_PRECISION_FP32 || c.precision == MOCR_PRECISION_BF16 ||
+          c.precision == MOCR_PRECISION_BF16X3,
+      "precision");
   req(c.sos_id >= 0 && c.sos_id < c.vocab && c.eos_id >= 0 && c.eos_id < c.vocab, "special ids");
 }
 
@@ -198,6 +200,9 @@ struct mocr_engine {
   float *img = nullptr, *X = nullptr, *X2 = nullptr, *XW = nullptr, *QKV = nullptr, *ATT = nullptr, *HID = nullptr;
   float *MEM = nullptr, *MEMKV = nullptr;
   size_t szX = 0, szXW = 0, szQKV = 0, szHID = 0;
+  // bf16 modes: hi/lo planes of the GEMM A operands and of every weight
+  uint16_t *XWh = nullptr, *XWl = nullptr, *ATTh = nullptr, *ATTl = nullptr, *HIDh = nullptr, *HIDl = nullptr;
+  uint16_t *MEMh = nullptr, *MEMl = nullptr, *dwh = nullptr, *dwl = nullptr, *kvwh = nullptr, *kvwl = nullptr;
   int cur_batch = 0;
   bool encoded = false;
   int partial_stage = -1;
@@ -229,7 +234,8 @@ struct mocr_engine {
     }
     void* bufs[] = {dw,      fcw_pad, fcb_pad, kvw_all, kvb_all, img,  X,        X2,       XW,     QKV,
                     ATT,     HID,     MEM,     MEMKV,   dx,      dq,   datt,     dy_sa,    dy_ca,  dy_ff, dh, dlogits,
-                    dlogits_hist, kcache, vcache, ids, feed, forced, finished, logp, st};
+                    dlogits_hist, kcache, vcache, ids, feed, forced, finished, logp, st, XWh, XWl, ATTh, ATTl,
+                    HIDh, HIDl, MEMh, MEMl, dwh, dwl, kvwh, kvwl};
     for (void* p : bufs)
       if (p) (void)hipFree(p);
     for (float* p : relbias)
@@ -292,6 +298,23 @@ struct mocr_engine {
     HID = dalloc<float>(szHID);
     MEM = dalloc<float>(B * M * d);
     MEMKV = dalloc<float>(B * M * L * 2 * d);
+    if (cfg.precision != MOCR_PRECISION_FP32) {
+      const bool x3 = cfg.precision == MOCR_PRECISION_BF16X3;
+      XWh = dalloc<uint16_t>(szXW);
+      ATTh = dalloc<uint16_t>(szXW);
+      HIDh = dalloc<uint16_t>(szHID);
+      MEMh = dalloc<uint16_t>(B * M * d);
+      dwh = dalloc<uint16_t>(lay->total);
+      kvwh = dalloc<uint16_t>(L * 2 * d * d);
+      if (x3) {
+        XWl = dalloc<uint16_t>(szXW);
+        ATTl = dalloc<uint16_t>(szXW);
+        HIDl = dalloc<uint16_t>(szHID);
+        MEMl = dalloc<uint16_t>(B * M * d);
+        dwl = dalloc<uint16_t>(lay->total);
+        kvwl = dalloc<uint16_t>(L * 2 * d * d);
+      }
+    }
 
     dx = dalloc<float>(B * d);
     dq = dalloc<float>(B * d);
@@ -347,6 +370,11 @@ struct mocr_engine {
                                hipMemcpyDeviceToDevice));
       MOCR_HIP_CHECK(hipMemcpy(kvb_all + (size_t)l * 2 * d, dw + w.ca_inb + d, 2 * d * sizeof(float),
                                hipMemcpyDeviceToDevice));
+    }
+    if (dwh) {
+      launch_split_bf16(dw, dwh, dwl, lay->total, stream);
+      launch_split_bf16(kvw_all, kvwh, kvwl, (size_t)cfg.n_layers * 2 * d * d, stream);
+      MOCR_HIP_CHECK(hipStreamSynchronize(stream));
     }
     MOCR_HIP_CHECK(hipDeviceSynchronize());
     weights_loaded = true;
@@ -406,11 +434,30 @@ struct mocr_engine {
   }
 
   // ---------------------------------------------------------------- encoder
-  void gemm(const char* name, const float* A, const float* Wt, const float* bias, float* C, int Mrows, int N, int K,
-            int epi, const WinGeom* wg, long alg_rows, int col_split = 0, size_t split_stride = 0) {
+  // A GEMM operand in the engine's precision: fp32, or bf16 hi (+ lo) planes.
+  struct Operand {
+    const float* f32;
+    const uint16_t* hi;
+    const uint16_t* lo;
+  };
+  Operand wop(size_t off) const { return {dw + off, dwh ? dwh + off : nullptr, dwl ? dwl + off : nullptr}; }
+  bool bf16_mode() const { return cfg.precision != MOCR_PRECISION_FP32; }
+
+  void gemm(const char* name, Operand A, Operand Wt, const float* bias, float* C, uint16_t* Ch, uint16_t* Cl,
+            int Mrows, int N, int K, int epi, const WinGeom* wg, long alg_rows, int col_split = 0,
+            size_t split_stride = 0) {
     GemmParams p{};
-    p.A = A;
-    p.W = Wt;
+    if (bf16_mode()) {
+      p.A = A.hi;
+      p.A_lo = A.lo;
+      p.W = Wt.hi;
+      p.W_lo = Wt.lo;
+      p.C16 = Ch;
+      p.C16lo = Cl;
+    } else {
+      p.A = A.f32;
+      p.W = Wt.f32;
+    }
     p.bias = bias;
     p.C = C;
     p.M = Mrows;
@@ -424,9 +471,15 @@ struct mocr_engine {
     p.col_split = col_split;
     p.split_stride = split_stride;
     const double flops = 2.0 * alg_rows * N * K;
-    const double bytes = 4.0 * ((double)alg_rows * K + (double)N * K + (double)alg_rows * N *
-                                                                            (epi == EPI_RESADD || epi == EPI_WINRES ? 2 : 1));
-    timed(name, flops, bytes, [&] { launch_gemm_f32(p, stream); });
+    const double ab = bf16_mode() ? (cfg.precision == MOCR_PRECISION_BF16X3 ? 4.0 : 2.0) : 4.0;
+    const double bytes = ab * ((double)alg_rows * K + (double)N * K) +
+                         4.0 * (double)alg_rows * N * (epi == EPI_RESADD || epi == EPI_WINRES ? 2 : 1);
+    timed(name, flops, bytes, [&] {
+      if (bf16_mode())
+        launch_gemm_bf16(p, stream);
+      else
+        launch_gemm_f32(p, stream);
+    });
   }
 
   // stop_after = k >= 0 stops after features[k] (0 = stem, 1..7 = stages/merges) and leaves
@@ -434,7 +487,6 @@ struct mocr_engine {
   void encode(int B, int stop_after = -1) {
     if (!weights_loaded) throw std::runtime_error("weights not loaded");
     if (B != cur_batch) throw std::runtime_error("batch differs from the uploaded images");
-    if (cfg.precision != MOCR_PRECISION_FP32) throw std::runtime_error("bf16 precision is not built yet");
     MOCR_HIP_CHECK(hipSetDevice(device));
     const size_t d = cfg.d_model, L = cfg.n_layers;
     timed("stem", 2.0 * B * H1 * W1 * kEmbed * 16, 4.0 * B * (cfg.img_h * cfg.img_w + (double)H1 * W1 * kEmbed),
@@ -448,6 +500,12 @@ struct mocr_engine {
     static const char* fc2_n[] = {"s1.fc2", "s2.fc2", "s3.fc2", "s4.fc2"};
     static const char* att_n[] = {"s1.wattn", "s2.wattn", "s3.wattn", "s4.wattn"};
     static const char* mrg_n[] = {"merge1", "merge2", "merge3"};
+    const bool b16 = bf16_mode();
+    // GEMM A operands: fp32 buffers, or their bf16 planes
+    float* xw32 = b16 ? nullptr : XW;
+    float* att32 = b16 ? nullptr : ATT;
+    float* hid32 = b16 ? nullptr : HID;
+    const Operand opXW{XW, XWh, XWl}, opATT{ATT, ATTh, ATTl}, opHID{HID, HIDh, HIDl};
     for (int s = 0; s < kStages; ++s) {
       const StageGeom& g = stage[s];
       const int C = g.C;
@@ -456,28 +514,40 @@ struct mocr_engine {
         const SwinBlockW& w = lay->blocks[bi];
         const WinGeom& wg = g.win[j & 1];
         const long wrows = (long)B * wg.nWin * kWinTok;
-        launch_ln_partition(X, W(w.n1w), W(w.n1b), XW, nullptr, B, C, wg, stream);
-        gemm(qkv_n[s], XW, W(w.qkvw), W(w.qkvb), QKV, (int)wrows, 3 * C, C, EPI_STORE, nullptr, rows);
-        timed(att_n[s], 4.0 * rows * kWinTok * C, 4.0 * (double)rows * 4 * C,
-              [&] { launch_window_attention(QKV, relbias[bi], ATT, nullptr, B, C, g.heads, wg, stream); });
-        gemm(proj_n[s], ATT, W(w.projw), W(w.projb), X, (int)wrows, C, C, EPI_WINRES, &wg, rows);
-        launch_layernorm(X, W(w.n2w), W(w.n2b), XW, nullptr, (int)rows, C, stream);
-        gemm(fc1_n[s], XW, W(w.fc1w), W(w.fc1b), HID, (int)rows, 4 * C, C, EPI_GELU, nullptr, rows);
-        gemm(fc2_n[s], HID, W(w.fc2w), W(w.fc2b), X, (int)rows, C, 4 * C, EPI_RESADD, nullptr, rows);
+        launch_ln_partition(X, W(w.n1w), W(w.n1b), xw32, XWh, XWl, B, C, wg, stream);
+        gemm(qkv_n[s], opXW, wop(w.qkvw), W(w.qkvb), QKV, nullptr, nullptr, (int)wrows, 3 * C, C, EPI_STORE, nullptr,
+             rows);
+        timed(att_n[s], 4.0 * rows * kWinTok * C, 4.0 * (double)rows * 4 * C, [&] {
+          launch_window_attention(QKV, relbias[bi], att32, ATTh, ATTl, B, C, g.heads, wg, stream);
+        });
+        gemm(proj_n[s], opATT, wop(w.projw), W(w.projb), X, nullptr, nullptr, (int)wrows, C, C, EPI_WINRES, &wg,
+             rows);
+        launch_layernorm(X, W(w.n2w), W(w.n2b), xw32, XWh, XWl, (int)rows, C, stream);
+        gemm(fc1_n[s], opXW, wop(w.fc1w), W(w.fc1b), hid32, HIDh, HIDl, (int)rows, 4 * C, C, EPI_GELU, nullptr,
+             rows);
+        gemm(fc2_n[s], opHID, wop(w.fc2w), W(w.fc2b), X, nullptr, nullptr, (int)rows, C, 4 * C, EPI_RESADD, nullptr,
+             rows);
       }
       if (stop_after == 1 + 2 * s) return finish_partial(1 + 2 * s);
       if (s < kStages - 1) {
         const MergeW& m = lay->merge[s];
         const long orow = (long)B * ((g.H + 1) / 2) * ((g.W + 1) / 2);
-        launch_merge_ln(X, W(m.nw), W(m.nb), XW, nullptr, B, g.H, g.W, C, stream);
-        gemm(mrg_n[s], XW, W(m.redw), nullptr, X2, (int)orow, 2 * C, 4 * C, EPI_STORE, nullptr, orow);
+        launch_merge_ln(X, W(m.nw), W(m.nb), xw32, XWh, XWl, B, g.H, g.W, C, stream);
+        gemm(mrg_n[s], opXW, wop(m.redw), nullptr, X2, nullptr, nullptr, (int)orow, 2 * C, 4 * C, EPI_STORE, nullptr,
+             orow);
         std::swap(X, X2);
         if (stop_after == 2 + 2 * s) return finish_partial(2 + 2 * s);
       }
     }
-    gemm("memproj", X, W(lay->projw), W(lay->projb), MEM, B * M, (int)d, kEncDim, EPI_STORE, nullptr, (long)B * M);
-    gemm("crosskv", MEM, kvw_all, kvb_all, MEMKV, B * M, (int)(L * 2 * d), (int)d, EPI_STORE, nullptr,
-         (long)B * M, (int)(2 * d), (size_t)cfg.max_batch * M * 2 * d);
+    Operand opX{X, nullptr, nullptr};
+    if (b16) {
+      launch_split_bf16(X, XWh, XWl, (size_t)B * M * kEncDim, stream);
+      opX = opXW;
+    }
+    gemm("memproj", opX, wop(lay->projw), W(lay->projb), MEM, MEMh, MEMl, B * M, (int)d, kEncDim, EPI_STORE, nullptr,
+         (long)B * M);
+    gemm("crosskv", Operand{MEM, MEMh, MEMl}, Operand{kvw_all, kvwh, kvwl}, kvb_all, MEMKV, nullptr, nullptr, B * M,
+         (int)(L * 2 * d), (int)d, EPI_STORE, nullptr, (long)B * M, (int)(2 * d), (size_t)cfg.max_batch * M * 2 * d);
     MOCR_HIP_CHECK(hipStreamSynchronize(stream));
     if (timing) flush_timing();
     encoded = true;

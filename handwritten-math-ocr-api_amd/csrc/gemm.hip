@@ -213,10 +213,216 @@ void launch_gemm_f32(const GemmParams& p, hipStream_t s) {
   MOCR_HIP_CHECK(hipGetLastError());
 }
 
+// ================================================================ bf16 MFMA path
+// v_mfma_f32_16x16x32_bf16 with fp32 accumulate.  PASSES = 1: plain bf16 operands.
+// PASSES = 3 ("bf16x3"): every fp32 operand x is carried as hi = bf16(x) and
+// lo = bf16(x - hi) and the product is hi·hi + hi·lo + lo·hi (the dropped lo·lo term
+// is ~2^-16 relative), i.e. near-fp32 accuracy on the bf16 matrix pipes.
+// Tile BM x BN x 32, 4 waves (2 x 2), wave tile (16 TM) x (16 TN); A/W planes are
+// staged global -> registers -> LDS with 80-B rows (16 rows of a ds_read_b128 group
+// land on 16 distinct 16-B slots).  MFMA operand maps: lane l holds
+// A[row l&15][k = 8(l>>4) + j], B[k][col l&15]; C/D: col = l&15, row = 4(l>>4) + r.
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int BK16 = 32;
+constexpr int LDS16 = BK16 + 8;  // 40 bf16 = 80 B per row
+
+__device__ __forceinline__ uint16_t bf16_rne(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+
+template <int EPI>
+__device__ __forceinline__ void epi_store16(const GemmParams& p, int row, int col, float v) {
+  if constexpr (EPI == EPI_RESADD || EPI == EPI_WINRES) {
+    epi_store<EPI>(p, row, col, v);  // fp32 residual stream
+  } else {
+    if (p.bias) v += p.bias[col];
+    if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
+    const size_t off = (size_t)row * p.ldc + col;
+    if (p.C) {
+      if (EPI == EPI_STORE && p.col_split) {
+        const int blk = col / p.col_split;
+        p.C[blk * p.split_stride + (size_t)row * p.col_split + (col - blk * p.col_split)] = v;
+      } else {
+        p.C[off] = v;
+      }
+    }
+    if (p.C16) {
+      const uint16_t hi = bf16_rne(v);
+      static_cast<uint16_t*>(p.C16)[off] = hi;
+      if (p.C16lo) static_cast<uint16_t*>(p.C16lo)[off] = bf16_rne(v - bf16_to_f32(hi));
+    }
+  }
+}
+
+template <int TM, int TN, int WGM, int WGN, int EPI, int PASSES>
+__global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_kernel(GemmParams p) {
+  constexpr int BM = 16 * TM * WGM;
+  constexpr int BN = 16 * TN * WGN;
+  constexpr int NT = 64 * WGM * WGN;
+  constexpr int PL = PASSES == 3 ? 2 : 1;  // planes per operand
+  constexpr int A_CHUNKS = BM * (BK16 / 8);  // 16-B chunks per plane
+  constexpr int W_CHUNKS = BN * (BK16 / 8);
+  constexpr int A_CH = (A_CHUNKS + NT - 1) / NT;  // per thread
+  constexpr int W_CH = (W_CHUNKS + NT - 1) / NT;
+
+  __shared__ uint16_t lds[PL * (BM + BN) * LDS16];
+  uint16_t* As[PL];
+  uint16_t* Ws[PL];
+#pragma unroll
+  for (int q = 0; q < PL; ++q) {
+    As[q] = lds + q * BM * LDS16;
+    Ws[q] = lds + PL * BM * LDS16 + q * BN * LDS16;
+  }
+  const uint16_t* Ag[2] = {static_cast<const uint16_t*>(p.A), static_cast<const uint16_t*>(p.A_lo)};
+  const uint16_t* Wg[2] = {static_cast<const uint16_t*>(p.W), static_cast<const uint16_t*>(p.W_lo)};
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WGN;
+  const int wn = wave % WGN;
+  const int row0 = blockIdx.y * BM;
+  const int col0 = blockIdx.x * BN;
+
+  u16x8 ra[PL][A_CH];
+  u16x8 rw[PL][W_CH];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < PL; ++q) {
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        const int idx = tid + i * NT;
+        const int r = idx >> 2;
+        const int c = (idx & 3) * 8;
+        const int gr = row0 + r;
+        ra[q][i] = (idx < A_CHUNKS && gr < p.M)
+                       ? *reinterpret_cast<const u16x8*>(Ag[q] + (size_t)gr * p.lda + k0 + c) : u16x8{};
+      }
+#pragma unroll
+      for (int i = 0; i < W_CH; ++i) {
+        const int idx = tid + i * NT;
+        const int r = idx >> 2;
+        const int c = (idx & 3) * 8;
+        rw[q][i] = idx < W_CHUNKS ? *reinterpret_cast<const u16x8*>(Wg[q] + (size_t)(col0 + r) * p.ldw + k0 + c)
+                                  : u16x8{};
+      }
+    }
+  };
+  auto sstore = [&]() {
+#pragma unroll
+    for (int q = 0; q < PL; ++q) {
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        const int idx = tid + i * NT;
+        if (idx < A_CHUNKS) *reinterpret_cast<u16x8*>(&As[q][(idx >> 2) * LDS16 + (idx & 3) * 8]) = ra[q][i];
+      }
+#pragma unroll
+      for (int i = 0; i < W_CH; ++i) {
+        const int idx = tid + i * NT;
+        if (idx < W_CHUNKS) *reinterpret_cast<u16x8*>(&Ws[q][(idx >> 2) * LDS16 + (idx & 3) * 8]) = rw[q][i];
+      }
+    }
+  };
+
+  floatx4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  gload(0);
+  sstore();
+  __syncthreads();
+  const int l16 = lane & 15;
+  const int kq = 8 * (lane >> 4);
+  for (int k0 = 0; k0 < p.K; k0 += BK16) {
+    const bool more = k0 + BK16 < p.K;
+    if (more) gload(k0 + BK16);
+    bf16x8 a[PL][TM], b[PL][TN];
+#pragma unroll
+    for (int q = 0; q < PL; ++q) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        a[q][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u16x8*>(
+                                                 &As[q][(wm * 16 * TM + i * 16 + l16) * LDS16 + kq]));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        b[q][j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u16x8*>(
+                                                 &Ws[q][(wn * 16 * TN + j * 16 + l16) * LDS16 + kq]));
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+        if constexpr (PASSES == 3) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+        }
+      }
+    __syncthreads();
+    if (more) {
+      sstore();
+      __syncthreads();
+    }
+  }
+
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + wm * 16 * TM + i * 16 + 4 * (lane >> 4) + r;
+        const int col = col0 + wn * 16 * TN + j * 16 + l16;
+        if (row < p.M) epi_store16<EPI>(p, row, col, acc[i][j][r]);
+      }
+}
+
+template <int TM, int TN, int WGM, int WGN, int PASSES>
+void launch_tile16(const GemmParams& p, hipStream_t s) {
+  constexpr int BM = 16 * TM * WGM;
+  constexpr int BN = 16 * TN * WGN;
+  dim3 grid(p.N / BN, (p.M + BM - 1) / BM);
+  dim3 block(64 * WGM * WGN);
+  switch (p.epi) {
+    case EPI_STORE: gemm_bf16_kernel<TM, TN, WGM, WGN, EPI_STORE, PASSES><<<grid, block, 0, s>>>(p); break;
+    case EPI_GELU: gemm_bf16_kernel<TM, TN, WGM, WGN, EPI_GELU, PASSES><<<grid, block, 0, s>>>(p); break;
+    case EPI_RESADD: gemm_bf16_kernel<TM, TN, WGM, WGN, EPI_RESADD, PASSES><<<grid, block, 0, s>>>(p); break;
+    case EPI_WINRES: gemm_bf16_kernel<TM, TN, WGM, WGN, EPI_WINRES, PASSES><<<grid, block, 0, s>>>(p); break;
+    default: throw std::runtime_error("gemm_bf16: bad epilogue");
+  }
+}
+
+template <int PASSES>
+void launch_bf16_passes(const GemmParams& p, hipStream_t s) {
+  if (p.N % 128 == 0) {
+    launch_tile16<4, 4, 2, 2, PASSES>(p, s);  // 128 x 128, waves of 64 x 64
+  } else if (p.N % 96 == 0) {
+    launch_tile16<4, 3, 2, 2, PASSES>(p, s);  // 128 x 96, waves of 64 x 48
+  } else {
+    throw std::runtime_error("gemm_bf16: N must be a multiple of 96 or 128");
+  }
+}
+
+}  // namespace
+
 void launch_gemm_bf16(const GemmParams& p, hipStream_t s) {
-  (void)p;
-  (void)s;
-  throw std::runtime_error("gemm_bf16: not built in this version");
+  if (p.K % BK16 != 0) throw std::runtime_error("gemm_bf16: K must be a multiple of 32");
+  if (p.M <= 0) return;
+  if (p.A_lo && p.W_lo) {
+    launch_bf16_passes<3>(p, s);
+  } else {
+    launch_bf16_passes<1>(p, s);
+  }
+  MOCR_HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace mocr

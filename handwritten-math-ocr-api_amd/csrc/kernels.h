@@ -27,11 +27,14 @@ struct WinGeom {
 };
 
 struct GemmParams {
-  const void* A;     // [M, lda] fp32 (precision 0) or bf16 (precision 1)
-  const void* W;     // [N, ldw] fp32 or bf16
+  const void* A;     // [M, lda] fp32 (gemm_f32) or bf16 hi plane (gemm_bf16)
+  const void* W;     // [N, ldw] fp32 or bf16 hi plane
+  const void* A_lo;  // bf16x3: lo planes (x - bf16(x)); nullptr for plain bf16
+  const void* W_lo;
   const float* bias; // [N] or nullptr
-  float* C;          // [M, ldc] (EPI_WINRES: X [B,H,W,ldc])
-  void* C16;         // optional bf16 copy of the output (EPI_STORE/EPI_GELU), may be null
+  float* C;          // [M, ldc] (EPI_WINRES: X [B,H,W,ldc]); may be null for EPI_STORE/GELU with C16
+  void* C16;         // optional bf16 hi plane of the output (EPI_STORE/EPI_GELU, gemm_bf16 only)
+  void* C16lo;       // optional bf16 lo plane of the output
   int M, N, K;
   int lda, ldw, ldc;
   int epi;
@@ -48,23 +51,27 @@ void launch_gemm_bf16(const GemmParams& p, hipStream_t s);
 void launch_stem(const float* img, const float* w, const float* b, const float* ln_w, const float* ln_b,
                  float* X, int B, int H, int W, hipStream_t s);
 
-// LayerNorm(norm1) + zero-pad + roll(-s) + window partition -> XW [B*nWin*49, C] (fp32 and/or bf16).
-void launch_ln_partition(const float* X, const float* g, const float* b, float* XW, uint16_t* XW16, int B, int C,
-                         const WinGeom& wg, hipStream_t s);
+// Outputs of the producers below: fp32 (Y) and/or bf16 hi plane (Yh) and/or lo plane
+// (Yl = bf16(y - hi)); each pointer may be null.
 
-// Plain row LayerNorm over C: Y[r] = LN(X[r]) (fp32 and/or bf16 outputs).
-void launch_layernorm(const float* X, const float* g, const float* b, float* Y, uint16_t* Y16, int rows, int C,
-                      hipStream_t s);
+// LayerNorm(norm1) + zero-pad + roll(-s) + window partition -> XW [B*nWin*49, C].
+void launch_ln_partition(const float* X, const float* g, const float* b, float* XW, uint16_t* XWh, uint16_t* XWl,
+                         int B, int C, const WinGeom& wg, hipStream_t s);
 
-// Window MSA: QKV [B*nWin*49, 3C] -> O [B*nWin*49, C] (fp32 and/or bf16 outputs).
-void launch_window_attention(const float* QKV, const float* relbias /*[heads,49,49]*/, float* O, uint16_t* O16,
-                             int B, int C, int heads, const WinGeom& wg, hipStream_t s);
+// Plain row LayerNorm over C: Y[r] = LN(X[r]).
+void launch_layernorm(const float* X, const float* g, const float* b, float* Y, uint16_t* Yh, uint16_t* Yl,
+                      int rows, int C, hipStream_t s);
+
+// Window MSA: QKV [B*nWin*49, 3C] fp32 -> O [B*nWin*49, C].
+void launch_window_attention(const float* QKV, const float* relbias /*[heads,49,49]*/, float* O, uint16_t* Oh,
+                             uint16_t* Ol, int B, int C, int heads, const WinGeom& wg, hipStream_t s);
 
 // PatchMerging gather (x0,x1,x2,x3 with zero pad) + LayerNorm(4C) -> Y [B*Ho*Wo, 4C].
-void launch_merge_ln(const float* X, const float* g, const float* b, float* Y, uint16_t* Y16, int B, int H, int W,
-                     int C, hipStream_t s);
+void launch_merge_ln(const float* X, const float* g, const float* b, float* Y, uint16_t* Yh, uint16_t* Yl, int B,
+                     int H, int W, int C, hipStream_t s);
 
-void launch_f32_to_bf16(const float* x, uint16_t* y, size_t n, hipStream_t s);
+// x -> bf16 hi (and lo) planes.
+void launch_split_bf16(const float* x, uint16_t* hi, uint16_t* lo, size_t n, hipStream_t s);
 
 // ------------------------------------------------------------------ decoder
 // Every decode kernel takes its step index t as an argument (one captured graph per

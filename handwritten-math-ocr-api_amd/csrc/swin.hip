@@ -43,15 +43,29 @@ __device__ __forceinline__ void ln_regs(float (&v)[NPER], int C, int lane, const
   }
 }
 
+// Row outputs: fp32 and/or bf16 hi plane and/or lo plane (x - bf16(x)), as the
+// consuming GEMM's precision needs.
+struct RowOut {
+  float* f32;
+  uint16_t* hi;
+  uint16_t* lo;
+};
+
+__device__ __forceinline__ void store_val(const RowOut& o, size_t off, float v) {
+  if (o.f32) o.f32[off] = v;
+  if (o.hi) {
+    const uint16_t h = f32_to_bf16_rne(v);
+    o.hi[off] = h;
+    if (o.lo) o.lo[off] = f32_to_bf16_rne(v - __uint_as_float((uint32_t)h << 16));
+  }
+}
+
 template <int NPER>
-__device__ __forceinline__ void store_row(float (&v)[NPER], int C, int lane, float* dst, uint16_t* dst16) {
+__device__ __forceinline__ void store_row(float (&v)[NPER], int C, int lane, const RowOut& o, size_t row_off) {
 #pragma unroll
   for (int i = 0; i < NPER; ++i) {
     const int c = lane + 64 * i;
-    if (c < C) {
-      if (dst) dst[c] = v[i];
-      if (dst16) dst16[c] = f32_to_bf16_rne(v[i]);
-    }
+    if (c < C) store_val(o, row_off + c, v[i]);
   }
 }
 
@@ -88,14 +102,14 @@ __global__ void __launch_bounds__(256) stem_kernel(const float* __restrict__ img
     v[i] = acc;
   }
   ln_regs<2>(v, 96, lane, g, beta);
-  store_row<2>(v, 96, lane, X + (size_t)tok * 96, nullptr);
+  store_row<2>(v, 96, lane, RowOut{X, nullptr, nullptr}, (size_t)tok * 96);
 }
 
 // ---------------------------------------------------------------- LN + window partition
 template <int NPER>
 __global__ void __launch_bounds__(256) ln_partition_kernel(const float* __restrict__ X, const float* __restrict__ g,
-                                                           const float* __restrict__ b, float* __restrict__ XW,
-                                                           uint16_t* __restrict__ XW16, int B, int C, WinGeom wg) {
+                                                           const float* __restrict__ b, RowOut out, int B, int C,
+                                                           WinGeom wg) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int per_img = wg.nWin * kWinTok;
@@ -111,8 +125,6 @@ __global__ void __launch_bounds__(256) ln_partition_kernel(const float* __restri
   if (y >= wg.pH) y -= wg.pH;
   if (x >= wg.pW) x -= wg.pW;
   float v[NPER];
-  float* dst = XW ? XW + (size_t)row * C : nullptr;
-  uint16_t* dst16 = XW16 ? XW16 + (size_t)row * C : nullptr;
   if (y < wg.H && x < wg.W) {
     const float* src = X + ((size_t)(bi * wg.H + y) * wg.W + x) * C;
 #pragma unroll
@@ -125,13 +137,12 @@ __global__ void __launch_bounds__(256) ln_partition_kernel(const float* __restri
 #pragma unroll
     for (int i = 0; i < NPER; ++i) v[i] = 0.f;  // F.pad after norm1: zero tokens
   }
-  store_row<NPER>(v, C, lane, dst, dst16);
+  store_row<NPER>(v, C, lane, out, (size_t)row * C);
 }
 
 template <int NPER>
 __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict__ X, const float* __restrict__ g,
-                                                        const float* __restrict__ b, float* __restrict__ Y,
-                                                        uint16_t* __restrict__ Y16, long rows, int C) {
+                                                        const float* __restrict__ b, RowOut out, long rows, int C) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -143,14 +154,14 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
     v[i] = c < C ? src[c] : 0.f;
   }
   ln_regs<NPER>(v, C, lane, g, b);
-  store_row<NPER>(v, C, lane, Y ? Y + (size_t)row * C : nullptr, Y16 ? Y16 + (size_t)row * C : nullptr);
+  store_row<NPER>(v, C, lane, out, (size_t)row * C);
 }
 
 // ---------------------------------------------------------------- PatchMerging + LN(4C)
 template <int NPER>
 __global__ void __launch_bounds__(256) merge_ln_kernel(const float* __restrict__ X, const float* __restrict__ g,
-                                                       const float* __restrict__ b, float* __restrict__ Y,
-                                                       uint16_t* __restrict__ Y16, int B, int H, int W, int C) {
+                                                       const float* __restrict__ b, RowOut out, int B, int H, int W,
+                                                       int C) {
   const int lane = threadIdx.x & 63;
   const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -175,7 +186,7 @@ __global__ void __launch_bounds__(256) merge_ln_kernel(const float* __restrict__
     v[i] = val;
   }
   ln_regs<NPER>(v, C4, lane, g, b);
-  store_row<NPER>(v, C4, lane, Y ? Y + (size_t)row * C4 : nullptr, Y16 ? Y16 + (size_t)row * C4 : nullptr);
+  store_row<NPER>(v, C4, lane, out, (size_t)row * C4);
 }
 
 // ---------------------------------------------------------------- window attention
@@ -193,8 +204,7 @@ constexpr int SP = 68;  // padded LDS row stride (floats): 16-B aligned, 17 slot
 
 __global__ void __launch_bounds__(256) window_attention_kernel(const float* __restrict__ QKV,
                                                                const float* __restrict__ relbias,
-                                                               float* __restrict__ O, uint16_t* __restrict__ O16,
-                                                               int C, WinGeom wg) {
+                                                               RowOut out, int C, WinGeom wg) {
   __shared__ float S[64 * SP];
   __shared__ float Vt[kHeadDim * SP];
   __shared__ int region[64];
@@ -321,18 +331,16 @@ __global__ void __launch_bounds__(256) window_attention_kernel(const float* __re
       const int row = bi * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
       if (row < kWinTok) {
         const float v = o[r] + red[(bi * 16 + r) * 64 + lane];
-        const size_t off = (base + row) * C + h * kHeadDim + l32;
-        if (O) O[off] = v;
-        if (O16) O16[off] = f32_to_bf16_rne(v);
+        store_val(out, (base + row) * C + h * kHeadDim + l32, v);
       }
     }
   }
 }
 
-__global__ void f32_to_bf16_kernel(const float* __restrict__ x, uint16_t* __restrict__ y, size_t n) {
+__global__ void split_bf16_kernel(const float* __restrict__ x, RowOut out, size_t n) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (; i < n; i += stride) y[i] = f32_to_bf16_rne(x[i]);
+  for (; i < n; i += stride) store_val(out, i, x[i]);
 }
 
 inline unsigned blocks_for_rows(long rows) { return (unsigned)((rows + 3) / 4); }
@@ -346,55 +354,58 @@ void launch_stem(const float* img, const float* w, const float* b, const float* 
   MOCR_HIP_CHECK(hipGetLastError());
 }
 
-void launch_ln_partition(const float* X, const float* g, const float* b, float* XW, uint16_t* XW16, int B, int C,
-                         const WinGeom& wg, hipStream_t s) {
+void launch_ln_partition(const float* X, const float* g, const float* b, float* XW, uint16_t* XWh, uint16_t* XWl,
+                         int B, int C, const WinGeom& wg, hipStream_t s) {
   const long rows = (long)B * wg.nWin * kWinTok;
+  const RowOut o{XW, XWh, XWl};
   switch ((C + 63) / 64) {
-    case 2: ln_partition_kernel<2><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, XW, XW16, B, C, wg); break;
-    case 3: ln_partition_kernel<3><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, XW, XW16, B, C, wg); break;
-    case 6: ln_partition_kernel<6><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, XW, XW16, B, C, wg); break;
-    case 12: ln_partition_kernel<12><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, XW, XW16, B, C, wg); break;
+    case 2: ln_partition_kernel<2><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, B, C, wg); break;
+    case 3: ln_partition_kernel<3><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, B, C, wg); break;
+    case 6: ln_partition_kernel<6><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, B, C, wg); break;
+    case 12: ln_partition_kernel<12><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, B, C, wg); break;
     default: throw std::runtime_error("ln_partition: unsupported C " + std::to_string(C));
   }
   MOCR_HIP_CHECK(hipGetLastError());
 }
 
-void launch_layernorm(const float* X, const float* g, const float* b, float* Y, uint16_t* Y16, int rows, int C,
-                      hipStream_t s) {
+void launch_layernorm(const float* X, const float* g, const float* b, float* Y, uint16_t* Yh, uint16_t* Yl,
+                      int rows, int C, hipStream_t s) {
+  const RowOut o{Y, Yh, Yl};
   switch ((C + 63) / 64) {
-    case 2: layernorm_kernel<2><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, Y, Y16, rows, C); break;
-    case 3: layernorm_kernel<3><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, Y, Y16, rows, C); break;
-    case 4: layernorm_kernel<4><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, Y, Y16, rows, C); break;
-    case 6: layernorm_kernel<6><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, Y, Y16, rows, C); break;
-    case 12: layernorm_kernel<12><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, Y, Y16, rows, C); break;
+    case 2: layernorm_kernel<2><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, rows, C); break;
+    case 3: layernorm_kernel<3><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, rows, C); break;
+    case 4: layernorm_kernel<4><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, rows, C); break;
+    case 6: layernorm_kernel<6><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, rows, C); break;
+    case 12: layernorm_kernel<12><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, rows, C); break;
     default: throw std::runtime_error("layernorm: unsupported C " + std::to_string(C));
   }
   MOCR_HIP_CHECK(hipGetLastError());
 }
 
-void launch_merge_ln(const float* X, const float* g, const float* b, float* Y, uint16_t* Y16, int B, int H, int W,
-                     int C, hipStream_t s) {
+void launch_merge_ln(const float* X, const float* g, const float* b, float* Y, uint16_t* Yh, uint16_t* Yl, int B,
+                     int H, int W, int C, hipStream_t s) {
+  const RowOut o{Y, Yh, Yl};
   const long rows = (long)B * ((H + 1) / 2) * ((W + 1) / 2);
   switch ((4 * C + 63) / 64) {
-    case 6: merge_ln_kernel<6><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, Y, Y16, B, H, W, C); break;
-    case 12: merge_ln_kernel<12><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, Y, Y16, B, H, W, C); break;
-    case 24: merge_ln_kernel<24><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, Y, Y16, B, H, W, C); break;
+    case 6: merge_ln_kernel<6><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, B, H, W, C); break;
+    case 12: merge_ln_kernel<12><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, B, H, W, C); break;
+    case 24: merge_ln_kernel<24><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, B, H, W, C); break;
     default: throw std::runtime_error("merge_ln: unsupported C " + std::to_string(C));
   }
   MOCR_HIP_CHECK(hipGetLastError());
 }
 
-void launch_window_attention(const float* QKV, const float* relbias, float* O, uint16_t* O16, int B, int C,
-                             int heads, const WinGeom& wg, hipStream_t s) {
+void launch_window_attention(const float* QKV, const float* relbias, float* O, uint16_t* Oh, uint16_t* Ol, int B,
+                             int C, int heads, const WinGeom& wg, hipStream_t s) {
   dim3 grid((unsigned)((long)B * wg.nWin), (unsigned)heads);
-  window_attention_kernel<<<grid, 256, 0, s>>>(QKV, relbias, O, O16, C, wg);
+  window_attention_kernel<<<grid, 256, 0, s>>>(QKV, relbias, RowOut{O, Oh, Ol}, C, wg);
   MOCR_HIP_CHECK(hipGetLastError());
 }
 
-void launch_f32_to_bf16(const float* x, uint16_t* y, size_t n, hipStream_t s) {
+void launch_split_bf16(const float* x, uint16_t* hi, uint16_t* lo, size_t n, hipStream_t s) {
   if (n == 0) return;
   const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 65536);
-  f32_to_bf16_kernel<<<blocks, 256, 0, s>>>(x, y, n);
+  split_bf16_kernel<<<blocks, 256, 0, s>>>(x, RowOut{nullptr, hi, lo}, n);
   MOCR_HIP_CHECK(hipGetLastError());
 }
 

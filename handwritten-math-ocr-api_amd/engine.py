@@ -20,7 +20,7 @@ from . import synth
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libmathocr.so")
 
-PRECISION = {"fp32": 0, "bf16": 1}
+PRECISION = {"fp32": 0, "bf16": 1, "bf16x3": 2}
 STOP = {"batch": 0, "none": 1}
 
 

@@ -43,8 +43,11 @@ extern "C" {
 
 /* Arithmetic of the engine. */
 enum {
-  MOCR_PRECISION_FP32 = 0, /* fp32 activations, fp32-input MFMA GEMMs: parity mode (token-exact) */
-  MOCR_PRECISION_BF16 = 1  /* bf16 MFMA encoder GEMMs with fp32 accumulate: throughput mode     */
+  MOCR_PRECISION_FP32 = 0,   /* fp32 everywhere; encoder GEMMs on fp32-input MFMA                     */
+  MOCR_PRECISION_BF16 = 1,   /* encoder GEMMs on bf16 MFMA (bf16 operands, fp32 accumulate); ~6e-3    */
+                             /* relative memory error, NOT token-exact                                */
+  MOCR_PRECISION_BF16X3 = 2  /* encoder GEMMs on bf16 MFMA with split operands x = hi + lo,            */
+                             /* hi*hi + hi*lo + lo*hi (~1e-5 relative); decoder fp32                  */
 };
 
 /* Greedy stopping rule (src/inference.py:23-25). */

@@ -143,3 +143,23 @@ def test_batch_invariance_384(pkg, g384):
     res = eng.decode(max_steps=g["meta"]["steps"], stop="none")
     np.testing.assert_array_equal(res.ids[0], g["ids"][1])
     eng.close()
+
+
+@pytest.mark.parametrize("precision,tol", [("bf16x3", 1e-4), ("bf16", 3e-2)])
+def test_bf16_encoder_modes(pkg, golden, precision, tol):
+    """bf16 MFMA encoder GEMMs: bf16x3 (split hi/lo operands) keeps fp32-level memory
+    error and the golden token ids; plain bf16 is checked for its looser error only."""
+    g = golden("g384_b2_pert")
+    m = g["meta"]
+    eng, _ = make_engine(pkg, m, precision=precision)
+    eng.encode(pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m["img_kind"]))
+    assert rel_err(eng.memory(), g["memory"]) < tol
+    res = eng.decode(max_steps=m["steps"], stop="none", forced=g["ids"], want_logits=True)
+    lerr = float(np.abs(res.logits[:, :g["logits"].shape[1]] - g["logits"]).max())
+    if precision == "bf16x3":
+        assert lerr < LOGIT_TOL, lerr
+        greedy = eng.decode(max_steps=m["steps"], stop="batch")
+        np.testing.assert_array_equal(greedy.ids, g["ids"])
+    else:
+        assert lerr < 0.05, lerr
+    eng.close()
