@@ -84,13 +84,11 @@ def main():
     imgs = torch.from_numpy(pkg.synth.make_images(B, H, W, seed0=1000 + rank * B)).to(f"cuda:{local}")
     eng.set_images(imgs)
     ids_local = torch.empty((B, S + 1), dtype=torch.int32, device=f"cuda:{local}")
-    ids_all = torch.empty((world * B, S + 1), dtype=torch.int32, device=f"cuda:{local}") if world > 1 else None
 
     def step():
         eng.encode()
         eng.decode_into(ids_local, max_steps=S, stop="none")
-        if world > 1:
-            dist.all_gather_into_tensor(ids_all, ids_local)
+        return pkg.parallel.gather_ids(ids_local, world)  # RCCL all-gather of the token streams
 
     for _ in range(args.warmup):
         step()

@@ -1,0 +1,57 @@
+"""CPU: the C-ABI library loads and exports what include/mathocr.h declares; host-side
+queries that do not touch the GPU."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    text = open(os.path.join(REPO, "include", "mathocr.h")).read()
+    return sorted(set(re.findall(r"\b(mocr_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_header_symbols_exported(pkg):
+    lib = pkg.load_library()
+    names = declared_symbols()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(lib, n), n
+    assert sorted(pkg.engine.exported_symbols()) == names
+    assert lib.mocr_abi_version() == 1
+
+
+def test_weight_count_matches_spec(pkg):
+    lib = pkg.load_library()
+    for vocab in (5075, 1000):
+        cfg = pkg.engine.make_config(img_hw=(384, 384), vocab=vocab)
+        n = lib.mocr_weight_count(ctypes.byref(cfg))
+        expect = sum(int(torch.tensor(s).prod()) for _, s, _, _ in pkg.synth.param_specs(vocab))
+        assert n == expect
+    cfg = pkg.engine.make_config(img_hw=(384, 384))
+    assert lib.mocr_weight_count(ctypes.byref(cfg)) == 36_679_757  # 37.45M minus unused swin.norm/head
+
+
+def test_memory_tokens(pkg):
+    lib = pkg.load_library()
+    for hw, m in (((384, 384), 144), ((96, 320), 30), ((224, 224), 49)):
+        cfg = pkg.engine.make_config(img_hw=hw)
+        assert lib.mocr_memory_tokens(ctypes.byref(cfg)) == m
+
+
+def test_bad_config_rejected(pkg):
+    lib = pkg.load_library()
+    cfg = pkg.engine.make_config(img_hw=(384, 384))
+    cfg.d_model = 512
+    assert lib.mocr_weight_count(ctypes.byref(cfg)) == 0
+    assert b"d_model" in lib.mocr_last_error(None)
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure path")
+def test_engine_fails_loudly_without_gpu(pkg):
+    with pytest.raises(pkg.MocrError):
+        pkg.Engine(img_hw=(96, 320), max_batch=1)

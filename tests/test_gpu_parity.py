@@ -163,3 +163,43 @@ def test_bf16_encoder_modes(pkg, golden, precision, tol):
     else:
         assert lerr < 0.05, lerr
     eng.close()
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+def test_serving_predict_matches_reference(pkg, golden, precision):
+    """im2latex.predict on the engine == the reference app/src/im2latex.py output
+    (formula string and confidence) for the EOS and the empty-output fixtures; the
+    batched predict gives the same per-image results."""
+    vocab, idx2char = pkg.synth.synthetic_vocab()
+    eng = pkg.Engine(img_hw=(96, 320), max_batch=4, precision=precision)
+    imgs, expected = [], []
+    for name in ("serve96x320_eos", "serve96x320_empty"):
+        m = golden(name)["meta"]
+        eng.load_weights(apply_eos_boost(pkg.synth.make_weights(m["seed"], m["variant"]), m["eos_boost"]))
+        img = pkg.synth.make_images(1, m["H"], m["W"], m["img_seed"], m["img_kind"])
+        formula, conf = pkg.im2latex.predict(eng, img, vocab, idx2char)
+        assert formula == m["formula"]
+        assert conf == pytest.approx(m["confidence"], rel=1e-4, abs=1e-7)
+        imgs.append(img)
+        expected.append((formula, conf))
+    # batched: both images under the EOS fixture's weights, vs single-image calls
+    m = golden("serve96x320_eos")["meta"]
+    eng.load_weights(apply_eos_boost(pkg.synth.make_weights(m["seed"], m["variant"]), m["eos_boost"]))
+    batch = np.concatenate(imgs + imgs[:1], 0)
+    got = pkg.im2latex.predict_batch(eng, batch, vocab, idx2char)
+    single = [pkg.im2latex.predict(eng, batch[i:i + 1], vocab, idx2char) for i in range(batch.shape[0])]
+    assert [g[0] for g in got] == [s[0] for s in single]
+    np.testing.assert_allclose([g[1] for g in got], [s[1] for s in single], rtol=1e-6)
+    assert got[0][0] == expected[0][0]
+    eng.close()
+
+
+def test_inference_predict_strings(pkg, golden):
+    """src/inference.py predict(): strings of the 96x320 batch fixture."""
+    g = golden("g96x320_b4_eos")
+    m = g["meta"]
+    vocab, idx2char = pkg.synth.synthetic_vocab()
+    eng, _ = make_engine(pkg, dict(m, B=3))  # max_batch 3 < 4 images: chunked decode
+    imgs = pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m["img_kind"])
+    assert pkg.inference.predict(imgs, eng, vocab, idx2char, "cuda") == m["strings"]
+    eng.close()
