@@ -39,10 +39,10 @@ def parse():
     ap.add_argument("--batch", type=int, default=64, help="images per GPU")
     ap.add_argument("--image", type=int, nargs=2, default=[384, 384])
     ap.add_argument("--tokens", type=int, default=128)
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3", "bf16"])
+    ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3", "bf16"])
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
-    ap.add_argument("--cpu-sample", type=int, default=8, help="images in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=32, help="images in the CPU-baseline sample")
     ap.add_argument("--no-b1-latency", dest="b1", action="store_false", default=True)
     return ap.parse_args()
 
