@@ -143,3 +143,35 @@ def test_shard_bounds(pkg):
         assert spans[0][0] == 0 and spans[-1][1] == n
         assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
         assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
+
+
+def test_replica_pool_imap_order_and_errors(pkg):
+    import threading
+    import time
+
+    class E:
+        def __init__(self, i):
+            self.i = i
+
+    pool = pkg.pipeline.ReplicaPool(engines=[E(0), E(1), E(2)])
+    seen = set()
+
+    def fn(eng, k):
+        seen.add(threading.get_ident())
+        time.sleep(0.01 * ((k * 7) % 3))
+        return k * 10, eng.i
+
+    out = list(pool.imap(fn, range(12)))
+    assert [o[0] for o in out] == [k * 10 for k in range(12)]
+    assert len({o[1] for o in out}) > 1  # work spread over replicas
+
+    def bad(eng, k):
+        if k == 4:
+            raise RuntimeError("boom")
+        return k
+
+    got = []
+    with pytest.raises(RuntimeError):
+        for v in pool.imap(bad, range(8)):
+            got.append(v)
+    assert got == [0, 1, 2, 3]
