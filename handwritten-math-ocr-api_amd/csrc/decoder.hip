@@ -9,9 +9,11 @@
 // function of the same inputs.
 //
 // Post-norm LayerNorms are never materialised: a sublayer writes its pre-norm sum
-// y = x + f(x), and every consumer of LN(y) (the next projection's A operand, the
-// next residual) normalises the rows it reads, from row statistics it computes itself
-// with one fixed reduction order, so all consumers see bit-identical LN(y).
+// y = x + f(x) plus, per row and 16-column slice, the slice's (mean, M2).  Every
+// consumer of LN(y) (the next projection's A operand, the next residual) merges the
+// 16 partials of a row in one fixed order (Chan et al.'s pairwise update) and
+// normalises the values it reads, so all consumers see bit-identical LN(y) without a
+// barrier or a re-read of the row.
 //
 // The step index t is a kernel argument (one captured hipGraph per chunk of 8 steps);
 // no kernel reads device state before issuing its loads.  With the batch-global stop,
@@ -29,53 +31,73 @@ __device__ __forceinline__ float ln_apply(float v, float mean, float rstd, float
   return fmaf((v - mean) * rstd, g, b);
 }
 
+// ------------------------------------------------------------------ row statistics
+constexpr int kSlices = kD / 16;  // 16-column slices per row
+
+// Pairwise merge of the (mean, M2) of two equal-size groups of n values each
+// (Chan et al.): mean = ma + d/2, M2 = qa + qb + d^2 n/2.  The 16 slice partials of a
+// row are merged as a fixed binary tree (n = 16, 32, 64, 128), lower group first, in
+// every kernel, so all consumers of a LayerNorm compute bit-identical statistics.
+__device__ __forceinline__ void merge_eq(float& m, float& q, float mb, float qb, float n) {
+  const float delta = mb - m;
+  q = q + qb + delta * delta * (n * 0.5f);
+  m = m + delta * 0.5f;
+}
+
+// Cross-lane tree level: this lane's group and its partner's (lane ^ mask) are merged
+// with the lower group first; both lanes get the same result.
+__device__ __forceinline__ void merge_lanes(float& m, float& q, int mask, bool upper, float n) {
+  const float mo = __shfl_xor(m, mask, 64);
+  const float qo = __shfl_xor(q, mask, 64);
+  if (upper) {
+    float mm = mo, qq = qo;
+    merge_eq(mm, qq, m, q, n);
+    m = mm;
+    q = qq;
+  } else {
+    merge_eq(m, q, mo, qo, n);
+  }
+}
+
+__device__ __forceinline__ float rstd_of(float m2) { return 1.0f / sqrtf(m2 * (1.0f / kD) + 1e-5f); }
+
+// Layout 1 (A-operand prologue): the 4 lanes g = 0..3 of a row each load 4 slices
+// (part[4g..4g+3]); levels 1-2 in-lane, levels 3-4 across lanes (lane ^ 16, ^ 32).
+__device__ __forceinline__ void row_stats_4lanes(const float* __restrict__ part, int g, float& mean, float& rstd) {
+  const floatx4 p0 = *reinterpret_cast<const floatx4*>(part + 8 * g);
+  const floatx4 p1 = *reinterpret_cast<const floatx4*>(part + 8 * g + 4);
+  float m = p0[0], q = p0[1], m2 = p1[0], q2 = p1[1];
+  merge_eq(m, q, p0[2], p0[3], 16.f);
+  merge_eq(m2, q2, p1[2], p1[3], 16.f);
+  merge_eq(m, q, m2, q2, 32.f);
+  merge_lanes(m, q, 16, (g & 1) != 0, 64.f);
+  merge_lanes(m, q, 32, (g & 2) != 0, 128.f);
+  mean = m;
+  rstd = rstd_of(q);
+}
+
+// Layout 2 (epilogue): the 16 lanes c = 0..15 of a row each load slice c; levels 1-4
+// across lanes (lane ^ 1, ^ 2, ^ 4, ^ 8).  Same tree as layout 1.
+__device__ __forceinline__ void row_stats_16lanes(const float* __restrict__ part, int c, float& mean, float& rstd) {
+  float m = part[2 * c], q = part[2 * c + 1];
+  merge_lanes(m, q, 1, (c & 1) != 0, 16.f);
+  merge_lanes(m, q, 2, (c & 2) != 0, 32.f);
+  merge_lanes(m, q, 4, (c & 4) != 0, 64.f);
+  merge_lanes(m, q, 8, (c & 8) != 0, 128.f);
+  mean = m;
+  rstd = rstd_of(q);
+}
+
 // ------------------------------------------------------------------ small-M GEMM
 // out[B, N] = A[B, K] · W[N, K]^T + bias on v_mfma_f32_16x16x4_f32.  A workgroup
 // owns a 16x16 output tile; its 4 waves split K and combine through LDS in a fixed
 // order.  Each lane loads float4 runs of A and W straight into registers (no reuse
 // inside the workgroup, so no LDS staging); lane group g = lane>>4 feeds
 // k = 4g + s at MFMA step s.
-//
-// LN(A) / LN(resid) are fused: the 16 rows' statistics are reduced from fragments
-// that are already in registers (A's own fragments, or the resid rows loaded in the
-// same layout), two-pass mean / variance with a fixed order, so every consumer of a
-// LayerNorm gets bit-identical values.
-template <int NI>
-__device__ __forceinline__ void frag_ln_stats(const floatx4 (&f)[NI], float (*red)[16], int lane, int wave,
-                                              float& mean, float& rstd) {
-  const int row = lane & 15;
-  float ps = 0.f;
-#pragma unroll
-  for (int i = 0; i < NI; ++i)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) ps += f[i][s];
-  ps += __shfl_xor(ps, 16, 64);
-  ps += __shfl_xor(ps, 32, 64);
-  if (lane < 16) red[wave][row] = ps;
-  __syncthreads();
-  mean = (((red[0][row] + red[1][row]) + red[2][row]) + red[3][row]) * (1.0f / kD);
-  __syncthreads();
-  float pq = 0.f;
-#pragma unroll
-  for (int i = 0; i < NI; ++i)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const float t = f[i][s] - mean;
-      pq += t * t;
-    }
-  pq += __shfl_xor(pq, 16, 64);
-  pq += __shfl_xor(pq, 32, 64);
-  if (lane < 16) red[wave][row] = pq;
-  __syncthreads();
-  const float var = (((red[0][row] + red[1][row]) + red[2][row]) + red[3][row]) * (1.0f / kD);
-  rstd = 1.0f / sqrtf(var + 1e-5f);
-}
-
 template <int EPI, int KW, bool ALN, bool RLN>
 __global__ void __launch_bounds__(256) rowgemm_kernel(RowGemmParams p) {
   const int t = p.t;
   constexpr int NI = KW / 16;
-  constexpr int NR = kD / 4 / 16;  // resid fragments per lane (d split over 4 waves)
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -87,46 +109,42 @@ __global__ void __launch_bounds__(256) rowgemm_kernel(RowGemmParams p) {
   const int kbeg = wave * KW;
   const bool row_ok = ra < p.B;
 
+  // issue every independent load first: A, W, LayerNorm affine, residual
   floatx4 a[NI], b[NI];
+  floatx4 gg[ALN ? NI : 1], bb[ALN ? NI : 1];
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     const int k = kbeg + i * 16 + 4 * g;
     a[i] = row_ok ? *reinterpret_cast<const floatx4*>(p.A + (size_t)ra * p.K + k) : floatx4{0.f, 0.f, 0.f, 0.f};
     b[i] = *reinterpret_cast<const floatx4*>(p.W + (size_t)cb * p.K + k);
-  }
-  floatx4 rf[RLN ? NR : 1];
-  if constexpr (RLN) {
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int k = wave * (kD / 4) + i * 16 + 4 * g;
-      rf[i] = row_ok ? *reinterpret_cast<const floatx4*>(p.resid + (size_t)ra * p.ldo + k)
-                     : floatx4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (ALN) {
+      gg[i] = *reinterpret_cast<const floatx4*>(p.a_ln_g + k);
+      bb[i] = *reinterpret_cast<const floatx4*>(p.a_ln_b + k);
     }
   }
-
-  __shared__ float red_s[4][16];
-  __shared__ float rn[16][kD + 1];
+  const int row = tid >> 4;
+  const int col = tid & 15;
+  const int grow = r0 + row;
+  const int gcol = c0 + col;
+  const bool out_ok = grow < p.B && gcol < p.n_valid;
+  float rres = 0.f, rg = 0.f, rb = 0.f;
+  if constexpr (EPI == DEC_RESADD) {
+    if (out_ok) {
+      rres = p.resid[(size_t)grow * p.ldo + gcol];
+      if constexpr (RLN) {
+        rg = p.r_ln_g[gcol];
+        rb = p.r_ln_b[gcol];
+      }
+    }
+  }
   if constexpr (ALN) {
+    const size_t srow = (size_t)(row_ok ? ra : 0) * 2 * kSlices;
     float mean, rstd;
-    frag_ln_stats<NI>(a, red_s, lane, wave, mean, rstd);
+    row_stats_4lanes(p.a_stats + srow, g, mean, rstd);
 #pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int k = kbeg + i * 16 + 4 * g;
-      const floatx4 gg = *reinterpret_cast<const floatx4*>(p.a_ln_g + k);
-      const floatx4 bb = *reinterpret_cast<const floatx4*>(p.a_ln_b + k);
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) a[i][s] = row_ok ? ln_apply(a[i][s], mean, rstd, gg[s], bb[s]) : 0.f;
-    }
-  }
-  if constexpr (RLN) {
-    float mean, rstd;
-    frag_ln_stats<NR>(rf, red_s, lane, wave, mean, rstd);
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int k = wave * (kD / 4) + i * 16 + 4 * g;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) rn[lane & 15][k + s] = ln_apply(rf[i][s], mean, rstd, p.r_ln_g[k + s], p.r_ln_b[k + s]);
-    }
+      for (int s = 0; s < 4; ++s) a[i][s] = row_ok ? ln_apply(a[i][s], mean, rstd, gg[i][s], bb[i][s]) : 0.f;
   }
 
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -139,11 +157,12 @@ __global__ void __launch_bounds__(256) rowgemm_kernel(RowGemmParams p) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) red[wave][g * 4 + r][lane & 15] = acc[r];
   __syncthreads();
-  const int row = tid >> 4;
-  const int col = tid & 15;
-  const int grow = r0 + row;
-  const int gcol = c0 + col;
-  if (grow >= p.B || gcol >= p.n_valid || dec_skip(p.st, t)) return;
+  if constexpr (EPI == DEC_RESADD && RLN) {  // all 16 lanes of a row take part in the merge
+    float mean, rstd;
+    row_stats_16lanes(p.r_stats + (size_t)(grow < p.B ? grow : 0) * 2 * kSlices, col, mean, rstd);
+    rres = ln_apply(rres, mean, rstd, rg, rb);
+  }
+  if (!out_ok || dec_skip(p.st, t)) return;  // uniform per 16-lane row group
   float v = ((red[0][row][col] + red[1][row][col]) + red[2][row][col]) + red[3][row][col];
   v += p.bias[gcol];
   if constexpr (EPI == DEC_STORE) {
@@ -151,8 +170,25 @@ __global__ void __launch_bounds__(256) rowgemm_kernel(RowGemmParams p) {
   } else if constexpr (EPI == DEC_RELU) {
     p.out[(size_t)grow * p.ldo + gcol] = fmaxf(v, 0.f);
   } else if constexpr (EPI == DEC_RESADD) {
-    const float r = RLN ? rn[row][gcol] : p.resid[(size_t)grow * p.ldo + gcol];
-    p.out[(size_t)grow * p.ldo + gcol] = r + v;
+    const float y = rres + v;
+    p.out[(size_t)grow * p.ldo + gcol] = y;
+    // (mean, M2) of this row's 16-column slice, reduced over the 16 lanes of the row
+    float s = y;
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    s += __shfl_xor(s, 8, 64);
+    const float m16 = s * (1.0f / 16);
+    float q = (y - m16) * (y - m16);
+    q += __shfl_xor(q, 1, 64);
+    q += __shfl_xor(q, 2, 64);
+    q += __shfl_xor(q, 4, 64);
+    q += __shfl_xor(q, 8, 64);
+    if (col == 0) {
+      float* so = p.out_stats + ((size_t)grow * kSlices + blockIdx.x) * 2;
+      so[0] = m16;
+      so[1] = q;
+    }
   } else if constexpr (EPI == DEC_QKV) {
     if (gcol < p.d) {
       p.out[(size_t)grow * p.d + gcol] = v;
@@ -182,7 +218,9 @@ template <int EPI>
 void launch_rowgemm_e(const RowGemmParams& p, dim3 grid, hipStream_t s) {
   const bool aln = p.a_ln_g != nullptr, rln = p.r_ln_g != nullptr;
   if (aln && rln) throw std::runtime_error("rowgemm: LayerNorm on both A and resid is not built");
-  if (aln && p.K != kD) throw std::runtime_error("rowgemm: LayerNorm prologue needs K == d_model");
+  if (aln && (p.K != kD || !p.a_stats)) throw std::runtime_error("rowgemm: LayerNorm prologue needs K == d, stats");
+  if (rln && !p.r_stats) throw std::runtime_error("rowgemm: residual LayerNorm needs stats");
+  if (EPI == DEC_RESADD && (p.N != kD || !p.out_stats)) throw std::runtime_error("rowgemm: RESADD writes d + stats");
   if (aln) {
     launch_rowgemm_k<EPI, true, false>(p, grid, s);
   } else if (rln) {
@@ -204,25 +242,24 @@ __global__ void __launch_bounds__(256) dec_embed0_kernel(const int32_t* __restri
 
 // ------------------------------------------------------------------ attention
 // Newest position of row b against n keys, HB heads per workgroup (4 waves).  A key
-// row slice of HB*32 floats is read by 8*HB lanes (one float4 each), so one wave
-// instruction covers 64/(8*HB) keys with full 128-B head rows; scores q·k·1/sqrt(32)
-// are reduced over the 8 lanes of a head.  Softmax is exp(s - max) with the sum
-// applied at the end (Σ e v / Σ e), as in the CPU flash-attention SDPA kernel the
-// reference's F.multi_head_attention_forward reaches.
+// row slice of HB*32 floats is read by 8*HB lanes (one float4 each); every K and V row
+// load of a lane is issued up front.  Scores q·k·1/sqrt(32) are reduced over the 8
+// lanes of a head.  Each wave runs a softmax over its own keys (local max, exp, sum,
+// Σ e·v), and the 4 wave partials are merged after one barrier with the usual
+// rescaling by exp(m_w - m); the result is Σ e v / Σ e, normalised at the end as in
+// the CPU flash-attention SDPA kernel the reference's F.multi_head_attention_forward
+// reaches.
 template <int HB, int NIT>
 __global__ void __launch_bounds__(256) dec_attn_kernel(const DecodeState* st, int t, const float* __restrict__ q,
                                                        const float* __restrict__ K, const float* __restrict__ V,
-                                                       size_t kv_b_stride, int kv_row_stride, int n_fixed,
+                                                       size_t kv_b_stride, int kv_row_stride, int n,
                                                        float* __restrict__ out, int d) {
   constexpr int DIMS = 32 * HB;
   constexpr int LPR = DIMS / 4;  // lanes per key row
   constexpr int RPW = 64 / LPR;  // key rows per wave instruction
-  constexpr int MAXN = NIT * 4 * RPW;  // key rows per lane: NIT (upper bound)
-  __shared__ float S[HB][MAXN];
-  __shared__ float ssum[HB];
-  __shared__ floatx4 red[4][RPW][LPR];
+  __shared__ floatx4 po[4][LPR];
+  __shared__ float pm[4][HB], ps[4][HB];
 
-  const int n = n_fixed ? n_fixed : t + 1;
   const int b = blockIdx.x;
   const int hg = blockIdx.y;
   const int tid = threadIdx.x;
@@ -237,14 +274,12 @@ __global__ void __launch_bounds__(256) dec_attn_kernel(const DecodeState* st, in
   const float* Kb = K + (size_t)b * kv_b_stride + hg * DIMS + c4;
   const float* Vb = V + (size_t)b * kv_b_stride + hg * DIMS + c4;
   const int m_first = wave * RPW + rsub;
-  const int niter = (n + 4 * RPW - 1) / (4 * RPW);
 
-  // issue every K and V row load of this lane before using any of them
   floatx4 kk[NIT], vv[NIT];
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int m = m_first + it * 4 * RPW;
-    if (it < niter && m < n) {
+    if (m < n) {
       kk[it] = *reinterpret_cast<const floatx4*>(Kb + (size_t)m * kv_row_stride);
       vv[it] = *reinterpret_cast<const floatx4*>(Vb + (size_t)m * kv_row_stride);
     } else {
@@ -252,9 +287,10 @@ __global__ void __launch_bounds__(256) dec_attn_kernel(const DecodeState* st, in
       vv[it] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
   }
+  float sc[NIT];
+  float mx = -INFINITY;
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
-    const int m = m_first + it * 4 * RPW;
     float s = q4[0] * kk[it][0];
     s = fmaf(q4[1], kk[it][1], s);
     s = fmaf(q4[2], kk[it][2], s);
@@ -262,48 +298,54 @@ __global__ void __launch_bounds__(256) dec_attn_kernel(const DecodeState* st, in
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
     s += __shfl_xor(s, 4, 64);
-    if ((li & 7) == 0 && it < niter && m < n) S[hl][m] = s * kAttnScale;
+    s *= kAttnScale;
+    sc[it] = (m_first + it * 4 * RPW < n) ? s : -INFINITY;
+    mx = fmaxf(mx, sc[it]);
   }
-  __syncthreads();
-
-  for (int h = wave; h < HB; h += 4) {
-    float mx = -INFINITY;
-    for (int j = lane; j < n; j += 64) mx = fmaxf(mx, S[h][j]);
-    mx = wave_max(mx);
-    float sum = 0.f;
-    for (int j = lane; j < n; j += 64) {
-      const float e = expf(S[h][j] - mx);
-      S[h][j] = e;
-      sum += e;
-    }
-    sum = wave_sum(sum);
-    if (lane == 0) ssum[h] = sum;
-  }
-  __syncthreads();
-
-  floatx4 o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int m = m_first + it * 4 * RPW;
-    if (it < niter && m < n) {
-      const float pm = S[hl][m];
-      o[0] = fmaf(pm, vv[it][0], o[0]);
-      o[1] = fmaf(pm, vv[it][1], o[1]);
-      o[2] = fmaf(pm, vv[it][2], o[2]);
-      o[3] = fmaf(pm, vv[it][3], o[3]);
+  for (int o = LPR; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  float sum = 0.f;
+  floatx4 o4 = {0.f, 0.f, 0.f, 0.f};
+  if (mx != -INFINITY) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const float e = expf(sc[it] - mx);
+      sum += e;
+      o4[0] = fmaf(e, vv[it][0], o4[0]);
+      o4[1] = fmaf(e, vv[it][1], o4[1]);
+      o4[2] = fmaf(e, vv[it][2], o4[2]);
+      o4[3] = fmaf(e, vv[it][3], o4[3]);
     }
   }
-  red[wave][rsub][li] = o;
+#pragma unroll
+  for (int o = LPR; o < 64; o <<= 1) {
+    sum += __shfl_xor(sum, o, 64);
+    o4[0] += __shfl_xor(o4[0], o, 64);
+    o4[1] += __shfl_xor(o4[1], o, 64);
+    o4[2] += __shfl_xor(o4[2], o, 64);
+    o4[3] += __shfl_xor(o4[3], o, 64);
+  }
+  if (rsub == 0) {
+    po[wave][li] = o4;
+    if ((li & 7) == 0) {
+      pm[wave][hl] = mx;
+      ps[wave][hl] = sum;
+    }
+  }
   __syncthreads();
   if (tid < DIMS && !dec_skip(st, t)) {
-    const int l4 = tid / 4;
-    const int e = tid % 4;
-    float acc = 0.f;
+    const int h = tid / 32;
+    float m = pm[0][h];
 #pragma unroll
-    for (int w = 0; w < 4; ++w)
+    for (int w = 1; w < 4; ++w) m = fmaxf(m, pm[w][h]);
+    float num = 0.f, den = 0.f;
 #pragma unroll
-      for (int r = 0; r < RPW; ++r) acc += red[w][r][l4][e];
-    out[(size_t)b * d + hg * DIMS + tid] = acc / ssum[tid / 32];
+    for (int w = 0; w < 4; ++w) {
+      const float f = pm[w][h] == -INFINITY ? 0.f : expf(pm[w][h] - m);
+      num = fmaf(po[w][tid / 4][tid % 4], f, num);
+      den = fmaf(ps[w][h], f, den);
+    }
+    out[(size_t)b * d + hg * DIMS + tid] = num / den;
   }
 }
 
@@ -326,50 +368,57 @@ __global__ void __launch_bounds__(256) dec_argmax_kernel(DecodeState* st, int t,
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const float* L = logits + (hist_stride ? (size_t)t * hist_stride : 0) + (size_t)b * ldl;
-  float best = -INFINITY;
+  // one pass: running (max, first argmax, Σ exp(l - max)) per thread, then merged
+  float best = -INFINITY, sum = 0.f;
   int bidx = 0x7fffffff;
-  for (int j = tid; j < V; j += 256) {
-    const float v = L[j];
-    if (v > best) {
-      best = v;
-      bidx = j;
+  constexpr int CH = 8;  // loads in flight per thread
+  for (int j0 = tid; j0 < V; j0 += 256 * CH) {
+    float vals[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) vals[c] = (j0 + 256 * c < V) ? L[j0 + 256 * c] : -INFINITY;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const float v = vals[c];
+      if (v > best) {
+        sum = sum * expf(best - v) + 1.0f;
+        best = v;
+        bidx = j0 + 256 * c;
+      } else if (v != -INFINITY) {
+        sum += expf(v - best);
+      }
     }
   }
+  auto merge = [](float& b1, int& i1, float& s1, float b2, int i2, float s2) {
+    const float m = fmaxf(b1, b2);
+    const float f1 = b1 == -INFINITY ? 0.f : expf(b1 - m);
+    const float f2 = b2 == -INFINITY ? 0.f : expf(b2 - m);
+    s1 = s1 * f1 + s2 * f2;
+    if (b2 > b1 || (b2 == b1 && i2 < i1)) i1 = i2;
+    b1 = m;
+  };
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(best, o, 64);
+    const float ob = __shfl_xor(best, o, 64);
     const int oi = __shfl_xor(bidx, o, 64);
-    if (ov > best || (ov == best && oi < bidx)) {
-      best = ov;
-      bidx = oi;
-    }
+    const float os = __shfl_xor(sum, o, 64);
+    merge(best, bidx, sum, ob, oi, os);
   }
-  __shared__ float sv[4];
+  __shared__ float sv[4], ss[4];
   __shared__ int si_[4];
-  __shared__ float ss[4];
   __shared__ int s_next;
   if (lane == 0) {
     sv[wave] = best;
     si_[wave] = bidx;
+    ss[wave] = sum;
   }
   __syncthreads();
   best = sv[0];
   bidx = si_[0];
+  sum = ss[0];
 #pragma unroll
-  for (int w = 1; w < 4; ++w) {
-    if (sv[w] > best || (sv[w] == best && si_[w] < bidx)) {
-      best = sv[w];
-      bidx = si_[w];
-    }
-  }
-  float sum = 0.f;
-  for (int j = tid; j < V; j += 256) sum += expf(L[j] - best);
-  sum = wave_sum(sum);
-  if (lane == 0) ss[wave] = sum;
-  __syncthreads();
+  for (int w = 1; w < 4; ++w) merge(best, bidx, sum, sv[w], si_[w], ss[w]);
   if (dec_skip(stop_batch ? st : nullptr, t)) return;
   if (tid == 0) {
-    sum = ((ss[0] + ss[1]) + ss[2]) + ss[3];
     const int next = forced ? forced[(size_t)b * ld_ids + t + 1] : bidx;
     ids[(size_t)b * ld_ids + t + 1] = bidx;
     feed[(size_t)b * ld_ids + t + 1] = next;
@@ -419,18 +468,23 @@ void launch_dec_embed0(const int32_t* feed, int ld_ids, const float* emb, const 
 void launch_dec_attn(const DecodeState* st, int t, const float* q, const float* K, const float* V,
                      size_t kv_b_stride, int kv_row_stride, int n_fixed, int n_max, float* out, int B, int d,
                      int heads, hipStream_t s) {
-  constexpr int HB = 2;
+  constexpr int HB = 1;
   if (d != kD || heads * 32 != d) throw std::runtime_error("dec_attn: d_model 256 with 8 heads of 32");
-  if (n_max > 256) throw std::runtime_error("dec_attn: at most 256 keys");
-  const int nit = (n_max + 15) / 16;  // 16 key rows per workgroup pass (4 waves x 4 rows)
+  if (n_max > 256 || n_fixed < 1) throw std::runtime_error("dec_attn: 1..256 keys");
+  const int nit = (n_max + 31) / 32;  // 32 key rows per workgroup pass (4 waves x 8 rows)
   const dim3 grid(B, heads / HB);
-#define MOCR_ATTN(N) dec_attn_kernel<HB, N><<<grid, 256, 0, s>>>(st, t, q, K, V, kv_b_stride, kv_row_stride, n_fixed, out, d)
-  if (nit <= 2) MOCR_ATTN(2);
-  else if (nit <= 4) MOCR_ATTN(4);
-  else if (nit <= 8) MOCR_ATTN(8);
-  else if (nit <= 10) MOCR_ATTN(10);
-  else if (nit <= 12) MOCR_ATTN(12);
-  else MOCR_ATTN(16);
+#define MOCR_ATTN(N) \
+  dec_attn_kernel<HB, N><<<grid, 256, 0, s>>>(st, t, q, K, V, kv_b_stride, kv_row_stride, n_fixed, out, d)
+  switch (nit) {
+    case 1: MOCR_ATTN(1); break;
+    case 2: MOCR_ATTN(2); break;
+    case 3: MOCR_ATTN(3); break;
+    case 4: MOCR_ATTN(4); break;
+    case 5: MOCR_ATTN(5); break;
+    case 6: MOCR_ATTN(6); break;
+    case 7: MOCR_ATTN(7); break;
+    default: MOCR_ATTN(8); break;
+  }
 #undef MOCR_ATTN
   MOCR_HIP_CHECK(hipGetLastError());
 }

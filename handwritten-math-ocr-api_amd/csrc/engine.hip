@@ -210,6 +210,7 @@ struct mocr_engine {
   // decoder state
   float *dx = nullptr, *dq = nullptr, *datt = nullptr, *dh = nullptr, *dlogits = nullptr;
   float *dy_sa = nullptr, *dy_ca = nullptr, *dy_ff = nullptr;
+  float *ds_sa = nullptr, *ds_ca = nullptr, *ds_ff = nullptr;  // row-stat partials [B][16][2]
   float* dlogits_hist = nullptr;
   float *kcache = nullptr, *vcache = nullptr;
   int32_t *ids = nullptr, *feed = nullptr, *forced = nullptr, *finished = nullptr;
@@ -234,6 +235,7 @@ struct mocr_engine {
     }
     void* bufs[] = {dw,      fcw_pad, fcb_pad, kvw_all, kvb_all, img,  X,        X2,       XW,     QKV,
                     ATT,     HID,     MEM,     MEMKV,   dx,      dq,   datt,     dy_sa,    dy_ca,  dy_ff, dh, dlogits,
+                    ds_sa,   ds_ca,   ds_ff,
                     dlogits_hist, kcache, vcache, ids, feed, forced, finished, logp, st, XWh, XWl, ATTh, ATTl,
                     HIDh, HIDl, MEMh, MEMl, dwh, dwl, kvwh, kvwl};
     for (void* p : bufs)
@@ -322,6 +324,9 @@ struct mocr_engine {
     dy_sa = dalloc<float>(B * d);
     dy_ca = dalloc<float>(B * d);
     dy_ff = dalloc<float>(B * d);
+    ds_sa = dalloc<float>(B * 32);
+    ds_ca = dalloc<float>(B * 32);
+    ds_ff = dalloc<float>(B * 32);
     dh = dalloc<float>(B * cfg.d_ff);
     dlogits = dalloc<float>(B * Vpad);
     kcache = dalloc<float>(L * B * cfg.max_pos * d);
@@ -595,36 +600,42 @@ struct mocr_engine {
       const float* xin = l ? dy_ff : dx;
       const float* xin_g = l ? W(prev->n3w) : nullptr;
       const float* xin_b = l ? W(prev->n3b) : nullptr;
+      const float* xin_s = l ? ds_ff : nullptr;
       // self-attention block: y_sa = x + SA(x)
       RowGemmParams p = base();
-      p.A = xin; p.a_ln_g = xin_g; p.a_ln_b = xin_b; p.W = W(w.sa_inw); p.bias = W(w.sa_inb);
+      p.A = xin; p.a_ln_g = xin_g; p.a_ln_b = xin_b; p.a_stats = xin_s; p.W = W(w.sa_inw); p.bias = W(w.sa_inb);
       p.out = dq; p.kcache = kc; p.vcache = vc; p.N = 3 * d; p.K = d; p.ldo = d; p.n_valid = 3 * d;
       p.epi = DEC_QKV;
       launch_rowgemm(p, s);
       launch_dec_attn(stp, t, dq, kc, vc, (size_t)cfg.max_pos * d, d, t + 1, t + 1, datt, B, d, cfg.n_heads, s);
       p = base();
       p.A = datt; p.W = W(w.sa_ow); p.bias = W(w.sa_ob); p.out = dy_sa; p.resid = xin; p.r_ln_g = xin_g;
-      p.r_ln_b = xin_b; p.N = d; p.K = d; p.ldo = d; p.n_valid = d; p.epi = DEC_RESADD;
+      p.r_ln_b = xin_b; p.r_stats = xin_s; p.out_stats = ds_sa; p.N = d; p.K = d; p.ldo = d; p.n_valid = d;
+      p.epi = DEC_RESADD;
       launch_rowgemm(p, s);
       // cross-attention block: y_ca = LN1(y_sa) + MHA(LN1(y_sa), mem)
       p = base();
-      p.A = dy_sa; p.a_ln_g = W(w.n1w); p.a_ln_b = W(w.n1b); p.W = W(w.ca_inw); p.bias = W(w.ca_inb);
+      p.A = dy_sa; p.a_ln_g = W(w.n1w); p.a_ln_b = W(w.n1b); p.a_stats = ds_sa; p.W = W(w.ca_inw);
+      p.bias = W(w.ca_inb);
       p.out = dq; p.N = d; p.K = d; p.ldo = d; p.n_valid = d; p.epi = DEC_STORE;
       launch_rowgemm(p, s);
       const float* memk = MEMKV + l * kv_layer;
       launch_dec_attn(stp, t, dq, memk, memk + d, (size_t)M * 2 * d, 2 * d, M, M, datt, B, d, cfg.n_heads, s);
       p = base();
       p.A = datt; p.W = W(w.ca_ow); p.bias = W(w.ca_ob); p.out = dy_ca; p.resid = dy_sa; p.r_ln_g = W(w.n1w);
-      p.r_ln_b = W(w.n1b); p.N = d; p.K = d; p.ldo = d; p.n_valid = d; p.epi = DEC_RESADD;
+      p.r_ln_b = W(w.n1b); p.r_stats = ds_sa; p.out_stats = ds_ca; p.N = d; p.K = d; p.ldo = d; p.n_valid = d;
+      p.epi = DEC_RESADD;
       launch_rowgemm(p, s);
       // feed-forward block: y_ff = LN2(y_ca) + W2 relu(W1 LN2(y_ca))
       p = base();
-      p.A = dy_ca; p.a_ln_g = W(w.n2w); p.a_ln_b = W(w.n2b); p.W = W(w.l1w); p.bias = W(w.l1b); p.out = dh;
+      p.A = dy_ca; p.a_ln_g = W(w.n2w); p.a_ln_b = W(w.n2b); p.a_stats = ds_ca; p.W = W(w.l1w); p.bias = W(w.l1b);
+      p.out = dh;
       p.N = cfg.d_ff; p.K = d; p.ldo = cfg.d_ff; p.n_valid = cfg.d_ff; p.epi = DEC_RELU;
       launch_rowgemm(p, s);
       p = base();
       p.A = dh; p.W = W(w.l2w); p.bias = W(w.l2b); p.out = dy_ff; p.resid = dy_ca; p.r_ln_g = W(w.n2w);
-      p.r_ln_b = W(w.n2b); p.N = d; p.K = cfg.d_ff; p.ldo = d; p.n_valid = d; p.epi = DEC_RESADD;
+      p.r_ln_b = W(w.n2b); p.r_stats = ds_ca; p.out_stats = ds_ff; p.N = d; p.K = cfg.d_ff; p.ldo = d;
+      p.n_valid = d; p.epi = DEC_RESADD;
       launch_rowgemm(p, s);
     }
     const DecLayerW& last = lay->layers[L - 1];
@@ -632,6 +643,7 @@ struct mocr_engine {
     p.A = dy_ff;
     p.a_ln_g = W(last.n3w);
     p.a_ln_b = W(last.n3b);
+    p.a_stats = ds_ff;
     p.W = fcw_pad;
     p.bias = fcb_pad;
     p.out = hist ? dlogits_hist : dlogits;

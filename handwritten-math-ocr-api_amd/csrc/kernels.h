@@ -91,7 +91,10 @@ struct RowGemmParams {
   float* out;          // [B, ldo]
   const float* resid;  // DEC_RESADD: [B, ldo] (pre-LayerNorm sums when r_ln_g is set)
   const float* a_ln_g; const float* a_ln_b;  // A := LayerNorm(A) * g + b, fused prologue
+  const float* a_stats;                      // ... with A's row statistics partials [B][16][2]
   const float* r_ln_g; const float* r_ln_b;  // resid := LayerNorm(resid) * g + b
+  const float* r_stats;                      // ... with resid's row statistics partials
+  float* out_stats;    // DEC_RESADD: write (mean, M2) of each 16-column slice of every output row
   float* kcache;       // DEC_QKV: [B, max_pos, d] for this layer
   float* vcache;
   int B, N, K, ldo;

@@ -1,0 +1,111 @@
+// Per-kernel cost of each decode kernel of libmathocr.so, in a 200-long chain replayed
+// from a hipGraph (B = 64 rows, d = 256, max_pos = 150, M = 144, V = 5075, step t = 100).
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/decode_kernels_bench.hip
+//        -L handwritten-math-ocr-api_amd/lib -lmathocr -Wl,-rpath,$PWD/handwritten-math-ocr-api_amd/lib
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../handwritten-math-ocr-api_amd/csrc/kernels.h"
+
+using namespace mocr;
+
+#define CK(x)                                                           \
+  do {                                                                  \
+    hipError_t e = (x);                                                 \
+    if (e != hipSuccess) {                                              \
+      printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); \
+      return 1;                                                         \
+    }                                                                   \
+  } while (0)
+
+template <typename T>
+T* alloc(size_t n) {
+  void* p;
+  if (hipMalloc(&p, n * sizeof(T)) != hipSuccess) return nullptr;
+  hipMemset(p, 0, n * sizeof(T));
+  return (T*)p;
+}
+
+int main() {
+  const int B = 64, d = 256, P = 150, M = 144, V = 5075, Vp = 5088, t = 100, L = 8;
+  float* x = alloc<float>(B * 512);
+  float* y = alloc<float>(B * 512);
+  float* q = alloc<float>(B * d);
+  float* att = alloc<float>(B * d);
+  float* W = alloc<float>((size_t)Vp * 512);
+  float* bias = alloc<float>(Vp);
+  float* g = alloc<float>(512);
+  float* kc = alloc<float>((size_t)B * P * d);
+  float* vc = alloc<float>((size_t)B * P * d);
+  float* memkv = alloc<float>((size_t)L * B * M * 2 * d);
+  float* logits = alloc<float>((size_t)B * Vp);
+  int32_t* ids = alloc<int32_t>(B * 151);
+  int32_t* feed = alloc<int32_t>(B * 151);
+  int32_t* fin = alloc<int32_t>(B);
+  float* logp = alloc<float>(B * 150);
+  DecodeState* st = alloc<DecodeState>(1);
+  float* stats = alloc<float>(B * 32);
+  float* stats2 = alloc<float>(B * 32);
+  hipStream_t s;
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+
+  auto rg = [&](int epi, int N, int K, bool aln, bool rln) {
+    return [=](hipStream_t ss) {
+      RowGemmParams p{};
+      p.A = x; p.W = W; p.bias = bias; p.out = y; p.resid = q; p.kcache = kc; p.vcache = vc;
+      p.B = B; p.N = N; p.K = K; p.ldo = (epi == DEC_LOGITS) ? Vp : (epi == DEC_RELU ? 512 : d);
+      p.d = d; p.max_pos = P; p.n_valid = epi == DEC_LOGITS ? V : N; p.epi = epi; p.t = t; p.st = nullptr;
+      if (epi == DEC_LOGITS) p.out = logits;
+      if (aln) { p.a_ln_g = g; p.a_ln_b = g; p.a_stats = stats; }
+      if (rln) { p.r_ln_g = g; p.r_ln_b = g; p.r_stats = stats; }
+      p.out_stats = stats2;
+      launch_rowgemm(p, ss);
+    };
+  };
+  std::vector<std::pair<std::string, std::function<void(hipStream_t)>>> cases = {
+      {"qkv N768 K256 +LN(A)", rg(DEC_QKV, 768, 256, true, false)},
+      {"oproj N256 K256 +LN(res)", rg(DEC_RESADD, 256, 256, false, true)},
+      {"qproj N256 K256 +LN(A)", rg(DEC_STORE, 256, 256, true, false)},
+      {"ffn1 N512 K256 +LN(A)", rg(DEC_RELU, 512, 256, true, false)},
+      {"ffn2 N256 K512 +LN(res)", rg(DEC_RESADD, 256, 512, false, true)},
+      {"plain N256 K256", rg(DEC_STORE, 256, 256, false, false)},
+      {"logits N5088 K256 +LN(A)", rg(DEC_LOGITS, Vp, 256, true, false)},
+      {"self-attn t=100", [=](hipStream_t ss) {
+         launch_dec_attn(nullptr, t, q, kc, vc, (size_t)P * d, d, t + 1, t + 1, att, B, d, 8, ss);
+       }},
+      {"cross-attn M=144", [=](hipStream_t ss) {
+         launch_dec_attn(nullptr, t, q, memkv, memkv + d, (size_t)M * 2 * d, 2 * d, M, M, att, B, d, 8, ss);
+       }},
+      {"argmax+embed", [=](hipStream_t ss) {
+         launch_dec_argmax(st, t, 0, logits, 0, Vp, V, B, ids, feed, nullptr, 151, logp, fin, 2, 0, W, W, x, d, ss);
+       }},
+  };
+  const int chain = 200;
+  for (auto& c : cases) {
+    hipGraph_t graph;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < chain; ++i) c.second(s);
+    CK(hipStreamEndCapture(s, &graph));
+    hipGraphExec_t exec;
+    CK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    CK(hipGraphLaunch(exec, s));
+    CK(hipStreamSynchronize(s));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, s));
+    for (int r = 0; r < 5; ++r) CK(hipGraphLaunch(exec, s));
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("%-28s %.2f us per kernel\n", c.first.c_str(), ms * 1000.f / (5 * chain));
+    CK(hipGraphExecDestroy(exec));
+    CK(hipGraphDestroy(graph));
+  }
+  return 0;
+}
