@@ -70,7 +70,18 @@ def cpu_baseline(args, pkg):
                       f"full-prefix re-decode as src/inference.py, fp32 torch CPU, {dt:.1f} s"}
 
 
-def roofline(stats, dtype):
+def pmc_traffic(precision, cls):
+    """HBM bytes per launch of a kernel class from the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic_<precision>.json, written by tools/pmc_traffic.py: FETCH_SIZE x2
+    + WRITE_SIZE), or None when no such profile exists."""
+    path = os.path.join(REPO, "profiles", f"pmc_traffic_{precision}.json")
+    try:
+        return json.load(open(path))["classes"][cls]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def roofline(stats, dtype, precision):
     """Dominant encoder GEMM class by event-timed GPU time: algorithmic FLOP per launch /
     average launch duration, against the dense MFMA peak of the arithmetic."""
     gemms = {k: v for k, v in stats.items() if v["flops"] > 0 and "attn" not in k and k != "stem"}
@@ -80,7 +91,8 @@ def roofline(stats, dtype):
     achieved = flops / (avg_ms * 1e-3) / 1e12
     peak = PEAK[dtype]
     return {"kernel": f"gemm_{'f32' if dtype == 'f32' else 'bf16'}[{dtype}] {name}", "bound": "mfma",
-            "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
+            "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+            "traffic": pmc_traffic(precision, name),
             "avg_launch_ms": avg_ms, "flops_per_launch": flops,
             "algorithmic_bytes_per_launch": d["bytes"] / d["launches"]}
 
@@ -188,7 +200,7 @@ def main():
     if iso:
         out["p50_image_latency_unloaded_ms"] = iso["batch_latency_ms"]
         out["p50_image_latency_b1_ms"] = iso["b1_latency_ms"]
-        out["roofline"] = roofline(iso["stats"], dtype)
+        out["roofline"] = roofline(iso["stats"], dtype, args.precision)
         out["encoder_ms_per_batch_events"] = sum(v["total_ms"] for v in iso["stats"].values()) / 3
         out["kernel_classes"] = {k: {"launches": v["launches"], "avg_ms": v["total_ms"] / v["launches"],
                                      "tflops": v["flops"] / v["total_ms"] * 1e-9 if v["total_ms"] else None}

@@ -24,6 +24,18 @@ namespace {
 constexpr int BK = 32;
 constexpr int LDS_STRIDE = BK + 4;
 
+// XCD-aware tile order (1-D grid): workgroups b and b+8 are dispatched to the same XCD,
+// so logical tile L = (b % 8) * ceil(n/8) + b / 8 (bijective form for n % 8 != 0) gives
+// each XCD a contiguous range of row-panel-major tiles, and the N-tiles that share an A
+// row panel share that XCD's L2.  Placement only affects speed, never results.
+__device__ __forceinline__ void tile_of(int gx, int& tx, int& ty) {
+  const int n = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, q = n >> 3, r = n & 7;
+  const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  ty = L / gx;
+  tx = L - ty * gx;
+}
+
 template <int EPI>
 __device__ __forceinline__ void epi_store(const GemmParams& p, int row, int col, float v) {
   if (p.bias) v += p.bias[col];
@@ -78,8 +90,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_f32_kernel(GemmParams p) 
   const int wave = tid >> 6;
   const int wm = wave / WGN;
   const int wn = wave % WGN;
-  const int row0 = blockIdx.y * BM;
-  const int col0 = blockIdx.x * BN;
+  int tx, ty;
+  tile_of(p.N / BN, tx, ty);
+  const int row0 = ty * BM;
+  const int col0 = tx * BN;
   const float* A = static_cast<const float*>(p.A);
   const float* W = static_cast<const float*>(p.W);
 
@@ -187,7 +201,7 @@ template <int TM, int TN, int WGM, int WGN>
 void launch_tile(const GemmParams& p, hipStream_t s) {
   constexpr int BM = 32 * TM * WGM;
   constexpr int BN = 32 * TN * WGN;
-  dim3 grid(p.N / BN, (p.M + BM - 1) / BM);
+  dim3 grid((p.N / BN) * ((p.M + BM - 1) / BM));
   dim3 block(64 * WGM * WGN);
   switch (p.epi) {
     case EPI_STORE: gemm_f32_kernel<TM, TN, WGM, WGN, EPI_STORE><<<grid, block, 0, s>>>(p); break;
@@ -288,8 +302,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_kernel(GemmParams p)
   const int wave = tid >> 6;
   const int wm = wave / WGN;
   const int wn = wave % WGN;
-  const int row0 = blockIdx.y * BM;
-  const int col0 = blockIdx.x * BN;
+  int tx, ty;
+  tile_of(p.N / BN, tx, ty);
+  const int row0 = ty * BM;
+  const int col0 = tx * BN;
 
   u16x8 ra[PL][A_CH];
   u16x8 rw[PL][W_CH];
@@ -390,7 +406,7 @@ template <int TM, int TN, int WGM, int WGN, int PASSES>
 void launch_tile16(const GemmParams& p, hipStream_t s) {
   constexpr int BM = 16 * TM * WGM;
   constexpr int BN = 16 * TN * WGN;
-  dim3 grid(p.N / BN, (p.M + BM - 1) / BM);
+  dim3 grid((p.N / BN) * ((p.M + BM - 1) / BM));
   dim3 block(64 * WGM * WGN);
   switch (p.epi) {
     case EPI_STORE: gemm_bf16_kernel<TM, TN, WGM, WGN, EPI_STORE, PASSES><<<grid, block, 0, s>>>(p); break;
