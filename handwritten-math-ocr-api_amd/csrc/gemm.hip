@@ -15,6 +15,8 @@
 // loads are issued before the current tile's MFMAs.  Within a 16-deep k chunk,
 // lane half h feeds k = 8h + s at MFMA step s, so each lane reads 8 contiguous
 // floats (two ds_read_b128) per operand instead of 8 scattered ones.
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace mocr {
@@ -275,6 +277,76 @@ __device__ __forceinline__ void epi_store16(const GemmParams& p, int row, int co
   }
 }
 
+// Row-vector epilogue: 8 consecutive columns of one output row (col % 8 == 0), the same
+// arithmetic as epi_store/epi_store16 element by element, but 16/32-B loads and stores.
+template <int EPI>
+__device__ __forceinline__ void epi_vec8(const GemmParams& p, int row, int col, float (&v)[8]) {
+  if (p.bias) {
+    const floatx4 b0 = *reinterpret_cast<const floatx4*>(p.bias + col);
+    const floatx4 b1 = *reinterpret_cast<const floatx4*>(p.bias + col + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] += b0[e];
+      v[4 + e] += b1[e];
+    }
+  }
+  if constexpr (EPI == EPI_RESADD || EPI == EPI_WINRES) {
+    float* c;
+    if constexpr (EPI == EPI_RESADD) {
+      c = p.C + (size_t)row * p.ldc + col;
+    } else {
+      const WinGeom& g = p.win;
+      const int per_img = g.nWin * kWinTok;
+      const int b = row / per_img;
+      const int rem = row - b * per_img;
+      const int win = rem / kWinTok;
+      const int tk = rem - win * kWinTok;
+      const int wy = win / g.nWx;
+      const int wx = win - wy * g.nWx;
+      int y = wy * kWin + tk / kWin + g.sh;
+      int x = wx * kWin + tk % kWin + g.sw;
+      if (y >= g.pH) y -= g.pH;
+      if (x >= g.pW) x -= g.pW;
+      if (y >= g.H || x >= g.W) return;  // padding token: cropped
+      c = p.C + ((size_t)(b * g.H + y) * g.W + x) * p.ldc + col;
+    }
+    floatx4 r0 = *reinterpret_cast<const floatx4*>(c);
+    floatx4 r1 = *reinterpret_cast<const floatx4*>(c + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      r0[e] = r0[e] + v[e];
+      r1[e] = r1[e] + v[4 + e];
+    }
+    *reinterpret_cast<floatx4*>(c) = r0;
+    *reinterpret_cast<floatx4*>(c + 4) = r1;
+  } else {
+    if constexpr (EPI == EPI_GELU) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+    }
+    const size_t off = (size_t)row * p.ldc + col;
+    if (p.C) {
+      float* c = p.C + off;
+      if (EPI == EPI_STORE && p.col_split) {
+        const int blk = col / p.col_split;
+        c = p.C + blk * p.split_stride + (size_t)row * p.col_split + (col - blk * p.col_split);
+      }
+      *reinterpret_cast<floatx4*>(c) = floatx4{v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<floatx4*>(c + 4) = floatx4{v[4], v[5], v[6], v[7]};
+    }
+    if (p.C16) {
+      u16x8 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        hi[e] = bf16_rne(v[e]);
+        lo[e] = bf16_rne(v[e] - bf16_to_f32(hi[e]));
+      }
+      *reinterpret_cast<u16x8*>(static_cast<uint16_t*>(p.C16) + off) = hi;
+      if (p.C16lo) *reinterpret_cast<u16x8*>(static_cast<uint16_t*>(p.C16lo) + off) = lo;
+    }
+  }
+}
+
 template <int TM, int TN, int WGM, int WGN, int EPI, int PASSES>
 __global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_kernel(GemmParams p) {
   constexpr int BM = 16 * TM * WGM;
@@ -402,27 +474,194 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_kernel(GemmParams p)
       }
 }
 
-template <int TM, int TN, int WGM, int WGN, int PASSES>
+// ---------------------------------------------------------------- LDS-DMA ring version
+// The operand tiles go global -> LDS by global_load_lds (16 B per lane, no VGPR
+// staging) into a 3-stage ring, so two k-tiles are in flight while the MFMAs consume a
+// third.  One raw s_barrier per k-tile, with a counted vmcnt: the DMA of the newest
+// tiles stays in flight across it (hipcc's __syncthreads would drain it).  Rows are
+// 64 B (32 bf16); the 16-B chunk c of row r is stored at chunk c ^ f((r >> 2) & 3) with
+// f = {0, 2, 3, 1}, applied on the DMA's per-lane source address (the LDS side of a
+// DMA is lane-linear), which makes every ds_read_b128 lane group of the MFMA
+// fragment reads hit 16 distinct 16-B slots.
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ int swz(int r) { return (0x1320 >> (4 * ((r >> 2) & 3))) & 3; }  // {0,2,3,1}
+
+template <int TM, int TN, int WGM, int WGN, int EPI, int PASSES, int NSTAGE>
+__global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_ring_kernel(GemmParams p) {
+  constexpr int BM = 16 * TM * WGM;
+  constexpr int BN = 16 * TN * WGN;
+  constexpr int NW = WGM * WGN;
+  constexpr int PL = PASSES == 3 ? 2 : 1;
+  constexpr int ROWB = BK16 * 2;                 // 64 B per tile row
+  constexpr int A_BYTES = BM * ROWB, W_BYTES = BN * ROWB;
+  constexpr int STAGE = PL * (A_BYTES + W_BYTES);
+  static_assert(NSTAGE == 2 || NSTAGE == 3, "ring depth");
+  // 1-KB DMA pieces (16 rows) per wave per plane; when the pieces do not split evenly
+  // (BN = 96: 6 over 4 waves) the spare slots re-load the last piece, identical bytes to
+  // the same LDS place, so every wave issues the same count and one vmcnt fits all
+  constexpr int A_DMA = (BM / 16 + NW - 1) / NW;
+  constexpr int W_DMA = (BN / 16 + NW - 1) / NW;
+  constexpr int DMA_PER_TILE = PL * (A_DMA + W_DMA);  // per wave
+
+  // epilogue: each wave transposes its accumulators through a private LDS slab, 32 rows
+  // of its 16*TN columns at a time (row stride padded by 4 floats)
+  constexpr int EW = 16 * TN, ES = EW + 4, ER = 32;
+  constexpr int EPI_BYTES = NW * ER * ES * 4;
+  static_assert(TM % 2 == 0 && (ER * EW / 8) % 64 == 0, "epilogue split");
+  __shared__ __attribute__((aligned(16))) char lds[NSTAGE * STAGE > EPI_BYTES ? NSTAGE * STAGE : EPI_BYTES];
+  const char* Ag[2] = {static_cast<const char*>(p.A), static_cast<const char*>(p.A_lo)};
+  const char* Wg[2] = {static_cast<const char*>(p.W), static_cast<const char*>(p.W_lo)};
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WGN;
+  const int wn = wave % WGN;
+  int tx, ty;
+  tile_of(p.N / BN, tx, ty);
+  const int row0 = ty * BM;
+  const int col0 = tx * BN;
+  const int nk = p.K / BK16;
+
+  // per-lane DMA source: piece row = 16*piece + lane/4, chunk lane%4 (swizzled)
+  const int prow = lane >> 2;
+  const int pch = lane & 3;
+  auto issue = [&](int kt) {
+    char* st = lds + (kt % NSTAGE) * STAGE;
+    const int kb = kt * ROWB;
+#pragma unroll
+    for (int q = 0; q < PL; ++q) {
+#pragma unroll
+      for (int i = 0; i < A_DMA; ++i) {
+        const int pc = min(wave * A_DMA + i, BM / 16 - 1);
+        const int r = pc * 16 + prow;
+        const int gr = min(row0 + r, p.M - 1);
+        const char* src = Ag[q] + (size_t)gr * p.lda * 2 + kb + 16 * (pch ^ swz(r));
+        __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(st + q * A_BYTES + pc * 1024), 16, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < W_DMA; ++i) {
+        const int pc = min(wave * W_DMA + i, BN / 16 - 1);
+        const int r = pc * 16 + prow;
+        const char* src = Wg[q] + (size_t)(col0 + r) * p.ldw * 2 + kb + 16 * (pch ^ swz(r));
+        __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(st + PL * A_BYTES + q * W_BYTES + pc * 1024), 16, 0, 0);
+      }
+    }
+  };
+
+  floatx4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0);
+  if (NSTAGE == 3 && nk > 1) issue(1);
+  const int l16 = lane & 15;
+  const int kq = lane >> 4;  // 16-B chunk of the fragment (k = 8*kq .. 8*kq+7)
+  for (int kt = 0; kt < nk; ++kt) {
+    // retire tile kt's DMA (tile kt+1's may stay in flight), then make it visible to all waves
+    if (NSTAGE == 3 && kt + 1 < nk) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_PER_TILE) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    // into the stage every wave finished reading before the barrier
+    if (kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1);
+    const char* st = lds + (kt % NSTAGE) * STAGE;
+    bf16x8 a[PL][TM], b[PL][TN];
+#pragma unroll
+    for (int q = 0; q < PL; ++q) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * 16 * TM + i * 16 + l16;
+        a[q][i] = *reinterpret_cast<const bf16x8*>(st + q * A_BYTES + r * ROWB + 16 * (kq ^ swz(r)));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = wn * 16 * TN + j * 16 + l16;
+        b[q][j] = *reinterpret_cast<const bf16x8*>(st + PL * A_BYTES + q * W_BYTES + r * ROWB + 16 * (kq ^ swz(r)));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+        if constexpr (PASSES == 3) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+        }
+      }
+  }
+
+  __builtin_amdgcn_s_barrier();  // every wave is done reading the ring; no DMA in flight
+  float* ep = reinterpret_cast<float*>(lds) + wave * ER * ES;
+#pragma unroll
+  for (int h = 0; h < TM / 2; ++h) {
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ep[(i2 * 16 + 4 * kq + r) * ES + j * 16 + l16] = acc[2 * h + i2][j][r];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int it = 0; it < ER * EW / 8 / 64; ++it) {
+      const int idx = it * 64 + lane;
+      const int rr = idx / (EW / 8);
+      const int cc = idx - rr * (EW / 8);
+      const floatx4 v0 = *reinterpret_cast<const floatx4*>(ep + rr * ES + cc * 8);
+      const floatx4 v1 = *reinterpret_cast<const floatx4*>(ep + rr * ES + cc * 8 + 4);
+      float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      const int row = row0 + wm * 16 * TM + h * 32 + rr;
+      if (row < p.M) epi_vec8<EPI>(p, row, col0 + wn * EW + cc * 8, v);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+template <int TM, int TN, int WGM, int WGN, int PASSES, int RING>
 void launch_tile16(const GemmParams& p, hipStream_t s) {
   constexpr int BM = 16 * TM * WGM;
   constexpr int BN = 16 * TN * WGN;
   dim3 grid((p.N / BN) * ((p.M + BM - 1) / BM));
   dim3 block(64 * WGM * WGN);
+#define MOCR_G16(E)                                                                       \
+  if constexpr (RING > 0)                                                                 \
+    gemm_bf16_ring_kernel<TM, TN, WGM, WGN, E, PASSES, RING><<<grid, block, 0, s>>>(p);   \
+  else                                                                                    \
+    gemm_bf16_kernel<TM, TN, WGM, WGN, E, PASSES><<<grid, block, 0, s>>>(p);
   switch (p.epi) {
-    case EPI_STORE: gemm_bf16_kernel<TM, TN, WGM, WGN, EPI_STORE, PASSES><<<grid, block, 0, s>>>(p); break;
-    case EPI_GELU: gemm_bf16_kernel<TM, TN, WGM, WGN, EPI_GELU, PASSES><<<grid, block, 0, s>>>(p); break;
-    case EPI_RESADD: gemm_bf16_kernel<TM, TN, WGM, WGN, EPI_RESADD, PASSES><<<grid, block, 0, s>>>(p); break;
-    case EPI_WINRES: gemm_bf16_kernel<TM, TN, WGM, WGN, EPI_WINRES, PASSES><<<grid, block, 0, s>>>(p); break;
+    case EPI_STORE: MOCR_G16(EPI_STORE); break;
+    case EPI_GELU: MOCR_G16(EPI_GELU); break;
+    case EPI_RESADD: MOCR_G16(EPI_RESADD); break;
+    case EPI_WINRES: MOCR_G16(EPI_WINRES); break;
     default: throw std::runtime_error("gemm_bf16: bad epilogue");
   }
+#undef MOCR_G16
 }
 
 template <int PASSES>
 void launch_bf16_passes(const GemmParams& p, hipStream_t s) {
-  if (p.N % 128 == 0) {
-    launch_tile16<4, 4, 2, 2, PASSES>(p, s);  // 128 x 128, waves of 64 x 64
-  } else if (p.N % 96 == 0) {
-    launch_tile16<4, 3, 2, 2, PASSES>(p, s);  // 128 x 96, waves of 64 x 48
+  // MOCR_GEMM_RING = 0 (register staging) | 2 | 3 (LDS-DMA ring depth); A/B switch
+  static const int ring = getenv("MOCR_GEMM_RING") ? atoi(getenv("MOCR_GEMM_RING")) : 2;
+  if (p.N % 128 == 0) {  // 128 x 128, waves of 64 x 64
+    if (ring == 3)
+      launch_tile16<4, 4, 2, 2, PASSES, 3>(p, s);
+    else if (ring == 2)
+      launch_tile16<4, 4, 2, 2, PASSES, 2>(p, s);
+    else
+      launch_tile16<4, 4, 2, 2, PASSES, 0>(p, s);
+  } else if (p.N % 96 == 0) {  // 128 x 96, waves of 64 x 48
+    if (ring == 3)
+      launch_tile16<4, 3, 2, 2, PASSES, 3>(p, s);
+    else if (ring == 2)
+      launch_tile16<4, 3, 2, 2, PASSES, 2>(p, s);
+    else
+      launch_tile16<4, 3, 2, 2, PASSES, 0>(p, s);
   } else {
     throw std::runtime_error("gemm_bf16: N must be a multiple of 96 or 128");
   }
