@@ -189,7 +189,8 @@ struct mocr_engine {
 
   // weights
   float* dw = nullptr;
-  std::vector<float*> relbias;  // per Swin block [heads,49,49]
+  std::vector<float*> relbias;  // per Swin block [heads,49,49] (fp32 attention)
+  std::vector<float*> relmask;  // per Swin block [types][heads][64][64] (bf16 attention)
   float* fcw_pad = nullptr;
   float* fcb_pad = nullptr;
   float* kvw_all = nullptr;  // [L*2d, d] cross-attention k/v in_proj rows of every layer
@@ -242,6 +243,8 @@ struct mocr_engine {
       if (p) (void)hipFree(p);
     for (float* p : relbias)
       if (p) (void)hipFree(p);
+    for (float* p : relmask)
+      if (p) (void)hipFree(p);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -286,6 +289,10 @@ struct mocr_engine {
     relbias.assign(lay->blocks.size(), nullptr);
     for (size_t i = 0, bi = 0; i < (size_t)kStages; ++i)
       for (int j = 0; j < kDepth[i]; ++j, ++bi) relbias[bi] = dalloc<float>((size_t)kHeads[i] * kWinTok * kWinTok);
+    relmask.assign(lay->blocks.size(), nullptr);
+    if (cfg.precision != MOCR_PRECISION_FP32)
+      for (size_t i = 0, bi = 0; i < (size_t)kStages; ++i)
+        for (int j = 0; j < kDepth[i]; ++j, ++bi) relmask[bi] = dalloc<float>((size_t)4 * kHeads[i] * 64 * 64);
     fcw_pad = dalloc<float>((size_t)Vpad * d);
     fcb_pad = dalloc<float>(Vpad);
     kvw_all = dalloc<float>(L * 2 * d * d);
@@ -340,6 +347,36 @@ struct mocr_engine {
     st = dalloc<DecodeState>(1);
   }
 
+  // [type][h][64 q][64 key] table of the bf16 attention kernel: bias[h][q][key] plus the
+  // shifted-window mask (-100 across regions, torchvision shifted_window_attention) of
+  // window type (last window row, last window column), -inf on the padded keys 49..63,
+  // 0 on the padded query rows.  A window's region ids depend only on whether it is
+  // the last one along each axis: shift_region(7 w + p, P, s) = 0 for w < P/7 - 1, and
+  // 1 + (p >= 7 - s) for the last window (2 everywhere when s = 0).
+  void build_relmask(const std::vector<float>& rb, int h, const WinGeom& wg, float* dst) {
+    const bool masked = wg.sh + wg.sw > 0;
+    auto reg = [](int p, bool last, int sft) { return sft == 0 ? 2 : (last ? 1 + (p >= kWin - sft) : 0); };
+    std::vector<float> t((size_t)4 * h * 64 * 64, 0.f);
+    for (int type = 0; type < 4; ++type) {
+      const bool ly = type & 2, lx = type & 1;
+      for (int hh = 0; hh < h; ++hh)
+        for (int q = 0; q < kWinTok; ++q)
+          for (int k = 0; k < 64; ++k) {
+            float v = -INFINITY;
+            if (k < kWinTok) {
+              v = rb[((size_t)hh * kWinTok + q) * kWinTok + k];
+              if (masked) {
+                const int rq = 3 * reg(q / kWin, ly, wg.sh) + reg(q % kWin, lx, wg.sw);
+                const int rk = 3 * reg(k / kWin, ly, wg.sh) + reg(k % kWin, lx, wg.sw);
+                if (rq != rk) v += -100.0f;
+              }
+            }
+            t[(((size_t)type * h + hh) * 64 + q) * 64 + k] = v;
+          }
+    }
+    MOCR_HIP_CHECK(hipMemcpy(dst, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice));
+  }
+
   void load_weights(const float* blob, size_t n) {
     if (n != lay->total)
       throw std::runtime_error("weight blob has " + std::to_string(n) + " floats, expected " +
@@ -362,6 +399,7 @@ struct mocr_engine {
             for (int hh = 0; hh < h; ++hh) rb[((size_t)hh * kWinTok + i) * kWinTok + k] = table[idx * h + hh];
           }
         MOCR_HIP_CHECK(hipMemcpy(relbias[bi], rb.data(), rb.size() * sizeof(float), hipMemcpyHostToDevice));
+        if (relmask[bi]) build_relmask(rb, h, stage[s].win[j & 1], relmask[bi]);
       }
     }
     const size_t d = cfg.d_model, V = cfg.vocab;
@@ -447,6 +485,9 @@ struct mocr_engine {
   };
   Operand wop(size_t off) const { return {dw + off, dwh ? dwh + off : nullptr, dwl ? dwl + off : nullptr}; }
   bool bf16_mode() const { return cfg.precision != MOCR_PRECISION_FP32; }
+  int attn_passes() const {
+    return cfg.precision == MOCR_PRECISION_FP32 ? 0 : (cfg.precision == MOCR_PRECISION_BF16X3 ? 3 : 1);
+  }
 
   void gemm(const char* name, Operand A, Operand Wt, const float* bias, float* C, uint16_t* Ch, uint16_t* Cl,
             int Mrows, int N, int K, int epi, const WinGeom* wg, long alg_rows, int col_split = 0,
@@ -505,6 +546,9 @@ struct mocr_engine {
     static const char* fc2_n[] = {"s1.fc2", "s2.fc2", "s3.fc2", "s4.fc2"};
     static const char* att_n[] = {"s1.wattn", "s2.wattn", "s3.wattn", "s4.wattn"};
     static const char* mrg_n[] = {"merge1", "merge2", "merge3"};
+    static const char* ln1_n[] = {"s1.ln1", "s2.ln1", "s3.ln1", "s4.ln1"};
+    static const char* ln2_n[] = {"s1.ln2", "s2.ln2", "s3.ln2", "s4.ln2"};
+    static const char* mln_n[] = {"merge1.ln", "merge2.ln", "merge3.ln"};
     const bool b16 = bf16_mode();
     // GEMM A operands: fp32 buffers, or their bf16 planes
     float* xw32 = b16 ? nullptr : XW;
@@ -519,15 +563,18 @@ struct mocr_engine {
         const SwinBlockW& w = lay->blocks[bi];
         const WinGeom& wg = g.win[j & 1];
         const long wrows = (long)B * wg.nWin * kWinTok;
-        launch_ln_partition(X, W(w.n1w), W(w.n1b), xw32, XWh, XWl, B, C, wg, stream);
+        timed(ln1_n[s], 0, 8.0 * wrows * C,
+              [&] { launch_ln_partition(X, W(w.n1w), W(w.n1b), xw32, XWh, XWl, B, C, wg, stream); });
         gemm(qkv_n[s], opXW, wop(w.qkvw), W(w.qkvb), QKV, nullptr, nullptr, (int)wrows, 3 * C, C, EPI_STORE, nullptr,
              rows);
         timed(att_n[s], 4.0 * rows * kWinTok * C, 4.0 * (double)rows * 4 * C, [&] {
-          launch_window_attention(QKV, relbias[bi], att32, ATTh, ATTl, B, C, g.heads, wg, stream);
+          launch_window_attention(QKV, relbias[bi], relmask[bi], att32, ATTh, ATTl, B, C, g.heads, wg, attn_passes(),
+                                  stream);
         });
         gemm(proj_n[s], opATT, wop(w.projw), W(w.projb), X, nullptr, nullptr, (int)wrows, C, C, EPI_WINRES, &wg,
              rows);
-        launch_layernorm(X, W(w.n2w), W(w.n2b), xw32, XWh, XWl, (int)rows, C, stream);
+        timed(ln2_n[s], 0, 8.0 * rows * C,
+              [&] { launch_layernorm(X, W(w.n2w), W(w.n2b), xw32, XWh, XWl, (int)rows, C, stream); });
         gemm(fc1_n[s], opXW, wop(w.fc1w), W(w.fc1b), hid32, HIDh, HIDl, (int)rows, 4 * C, C, EPI_GELU, nullptr,
              rows);
         gemm(fc2_n[s], opHID, wop(w.fc2w), W(w.fc2b), X, nullptr, nullptr, (int)rows, C, 4 * C, EPI_RESADD, nullptr,
@@ -537,7 +584,8 @@ struct mocr_engine {
       if (s < kStages - 1) {
         const MergeW& m = lay->merge[s];
         const long orow = (long)B * ((g.H + 1) / 2) * ((g.W + 1) / 2);
-        launch_merge_ln(X, W(m.nw), W(m.nb), xw32, XWh, XWl, B, g.H, g.W, C, stream);
+        timed(mln_n[s], 0, 8.0 * orow * 4 * C,
+              [&] { launch_merge_ln(X, W(m.nw), W(m.nb), xw32, XWh, XWl, B, g.H, g.W, C, stream); });
         gemm(mrg_n[s], opXW, wop(m.redw), nullptr, X2, nullptr, nullptr, (int)orow, 2 * C, 4 * C, EPI_STORE, nullptr,
              orow);
         std::swap(X, X2);
@@ -546,7 +594,8 @@ struct mocr_engine {
     }
     Operand opX{X, nullptr, nullptr};
     if (b16) {
-      launch_split_bf16(X, XWh, XWl, (size_t)B * M * kEncDim, stream);
+      timed("split(memory)", 0, 8.0 * B * M * kEncDim,
+            [&] { launch_split_bf16(X, XWh, XWl, (size_t)B * M * kEncDim, stream); });
       opX = opXW;
     }
     gemm("memproj", opX, wop(lay->projw), W(lay->projb), MEM, MEMh, MEMl, B * M, (int)d, kEncDim, EPI_STORE, nullptr,

@@ -62,9 +62,12 @@ void launch_ln_partition(const float* X, const float* g, const float* b, float* 
 void launch_layernorm(const float* X, const float* g, const float* b, float* Y, uint16_t* Yh, uint16_t* Yl,
                       int rows, int C, hipStream_t s);
 
-// Window MSA: QKV [B*nWin*49, 3C] fp32 -> O [B*nWin*49, C].
-void launch_window_attention(const float* QKV, const float* relbias /*[heads,49,49]*/, float* O, uint16_t* Oh,
-                             uint16_t* Ol, int B, int C, int heads, const WinGeom& wg, hipStream_t s);
+// Window MSA: QKV [B*nWin*49, 3C] fp32 -> O [B*nWin*49, C].  passes 0: fp32 MFMA with
+// relbias [heads,49,49] and the region mask computed in-kernel; 1 / 3: bf16 / bf16x3
+// MFMA with relmask [types][heads][64][64] (bias + shift mask + -inf key padding; 4
+// window types for shifted blocks, 1 otherwise).
+void launch_window_attention(const float* QKV, const float* relbias, const float* relmask, float* O, uint16_t* Oh,
+                             uint16_t* Ol, int B, int C, int heads, const WinGeom& wg, int passes, hipStream_t s);
 
 // PatchMerging gather (x0,x1,x2,x3 with zero pad) + LayerNorm(4C) -> Y [B*Ho*Wo, 4C].
 void launch_merge_ln(const float* X, const float* g, const float* b, float* Y, uint16_t* Yh, uint16_t* Yl, int B,

@@ -337,6 +337,180 @@ __global__ void __launch_bounds__(256) window_attention_kernel(const float* __re
   }
 }
 
+// ---------------------------------------------------------------- window attention on bf16 MFMA
+// One wave per (window, head), no LDS, no block barrier (bf16 / bf16x3 precision modes).
+//   S^T = K Q^T   v_mfma_f32_16x16x32_bf16, tile (key tile kt, query tile qt), k = head dim:
+//                 A = K[key 16kt + l%16][8(l/16) .. +7], B = Q[q 16qt + l%16][same] -- both
+//                 are 8 contiguous floats of one QKV row, loaded straight from HBM.
+//   softmax over the keys of a query column: 16 values per lane (kt, r) + 4 lane groups.
+//   O^T = V^T P^T with k = keys permuted so that the B operand of k-step s is exactly the
+//                 P^T accumulators of key tiles 2s, 2s+1 (lane keys 4(l/16) + r, r = 0..3):
+//                 A = V[keys 32s + {0,16} + 4(l/16) + r][d 16dt + l%16].
+// `table` = [type][head][64 q][64 key] fp32: relative-position bias + shift mask for the
+// window type (last window row / column), -inf on the padded keys 49..63 (host-built,
+// engine.hip build_relmask).  PASSES = 3: hi*hi + hi*lo + lo*hi (bf16x3), 1: hi*hi.
+typedef __bf16 abf16x8 __attribute__((ext_vector_type(8)));
+typedef uint16_t au16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split8(const float (&x)[8], abf16x8& hi, abf16x8& lo) {
+  au16x8 h, l;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    h[e] = f32_to_bf16_rne(x[e]);
+    l[e] = f32_to_bf16_rne(x[e] - __uint_as_float((uint32_t)h[e] << 16));
+  }
+  hi = __builtin_bit_cast(abf16x8, h);
+  lo = __builtin_bit_cast(abf16x8, l);
+}
+
+template <int PASSES>
+__device__ __forceinline__ floatx4 mfma3(const abf16x8& ah, const abf16x8& al, const abf16x8& bh,
+                                         const abf16x8& bl, floatx4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
+  if constexpr (PASSES == 3) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
+  }
+  return c;
+}
+
+template <int PASSES>
+__global__ void __launch_bounds__(256) window_attention_mfma_kernel(const float* __restrict__ QKV,
+                                                                    const float* __restrict__ table, RowOut out,
+                                                                    int C, int heads, long npairs, WinGeom wg) {
+  const int lane = threadIdx.x & 63;
+  const long pair = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pair >= npairs) return;  // whole wave; nothing below synchronises across waves
+  const long win_g = pair / heads;
+  const int h = (int)(pair - win_g * heads);
+  const int l15 = lane & 15;
+  const int g = lane >> 4;
+  const int C3 = 3 * C;
+  const float* base = QKV + (size_t)win_g * kWinTok * C3 + h * kHeadDim;
+  const float scale = 0.17677669529663687f;  // 32 ** -0.5
+
+  abf16x8 kh[4], kl[4];
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt) {
+    const int key = 16 * kt + l15;
+    float x[8];
+    if (key < kWinTok) {
+      const floatx4 a = *reinterpret_cast<const floatx4*>(base + (size_t)key * C3 + C + 8 * g);
+      const floatx4 b = *reinterpret_cast<const floatx4*>(base + (size_t)key * C3 + C + 8 * g + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        x[e] = a[e];
+        x[4 + e] = b[e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = 0.f;
+    }
+    split8(x, kh[kt], kl[kt]);
+  }
+  abf16x8 vh[2][2], vl[2][2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int key = 32 * s + (j >> 2) * 16 + 4 * g + (j & 3);
+        x[j] = key < kWinTok ? base[(size_t)key * C3 + 2 * C + 16 * dt + l15] : 0.f;
+      }
+      split8(x, vh[dt][s], vl[dt][s]);
+    }
+
+  int type = 0;
+  if (wg.sh + wg.sw > 0) {
+    const int win = (int)(win_g % wg.nWin);
+    const int wy = win / wg.nWx;
+    const int wx = win - wy * wg.nWx;
+    type = 2 * (wy == wg.nWin / wg.nWx - 1) + (wx == wg.nWx - 1);
+  }
+  const float* tb = table + ((size_t)type * heads + h) * 64 * 64;
+
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {
+    const int q = 16 * qt + l15;
+    abf16x8 qh, ql;
+    {
+      float x[8];
+      if (q < kWinTok) {
+        const floatx4 a = *reinterpret_cast<const floatx4*>(base + (size_t)q * C3 + 8 * g);
+        const floatx4 b = *reinterpret_cast<const floatx4*>(base + (size_t)q * C3 + 8 * g + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          x[e] = a[e] * scale;
+          x[4 + e] = b[e] * scale;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = 0.f;
+      }
+      split8(x, qh, ql);
+    }
+    floatx4 st[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) st[kt] = mfma3<PASSES>(kh[kt], kl[kt], qh, ql, floatx4{0.f, 0.f, 0.f, 0.f});
+    // bias + mask (+ -inf on padded keys), then softmax over the query's 64 key slots
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      const floatx4 b = *reinterpret_cast<const floatx4*>(tb + q * 64 + 16 * kt + 4 * g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        st[kt][r] = st[kt][r] + b[r];
+        m = fmaxf(m, st[kt][r]);
+      }
+    }
+    m = fmaxf(m, __shfl_xor(m, 16));
+    m = fmaxf(m, __shfl_xor(m, 32));
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        st[kt][r] = expf(st[kt][r] - m);
+        sum += st[kt][r];
+      }
+    sum += __shfl_xor(sum, 16);
+    sum += __shfl_xor(sum, 32);
+    abf16x8 ph[2], pl[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = st[2 * s + (j >> 2)][j & 3] / sum;
+      split8(x, ph[s], pl[s]);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      floatx4 o = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) o = mfma3<PASSES>(vh[dt][s], vl[dt][s], ph[s], pl[s], o);
+      if (q < kWinTok) {
+        const size_t off = ((size_t)win_g * kWinTok + q) * C + h * kHeadDim + 16 * dt + 4 * g;
+        if (out.f32) *reinterpret_cast<floatx4*>(out.f32 + off) = o;
+        if (out.hi) {
+          uint16_t hs[4], ls[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            hs[r] = f32_to_bf16_rne(o[r]);
+            ls[r] = f32_to_bf16_rne(o[r] - __uint_as_float((uint32_t)hs[r] << 16));
+          }
+          *reinterpret_cast<uint2*>(out.hi + off) =
+              make_uint2(hs[0] | ((uint32_t)hs[1] << 16), hs[2] | ((uint32_t)hs[3] << 16));
+          if (out.lo)
+            *reinterpret_cast<uint2*>(out.lo + off) =
+                make_uint2(ls[0] | ((uint32_t)ls[1] << 16), ls[2] | ((uint32_t)ls[3] << 16));
+        }
+      }
+    }
+  }
+}
+
 __global__ void split_bf16_kernel(const float* __restrict__ x, RowOut out, size_t n) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -395,10 +569,21 @@ void launch_merge_ln(const float* X, const float* g, const float* b, float* Y, u
   MOCR_HIP_CHECK(hipGetLastError());
 }
 
-void launch_window_attention(const float* QKV, const float* relbias, float* O, uint16_t* Oh, uint16_t* Ol, int B,
-                             int C, int heads, const WinGeom& wg, hipStream_t s) {
-  dim3 grid((unsigned)((long)B * wg.nWin), (unsigned)heads);
-  window_attention_kernel<<<grid, 256, 0, s>>>(QKV, relbias, RowOut{O, Oh, Ol}, C, wg);
+void launch_window_attention(const float* QKV, const float* relbias, const float* relmask, float* O, uint16_t* Oh,
+                             uint16_t* Ol, int B, int C, int heads, const WinGeom& wg, int passes, hipStream_t s) {
+  if (passes == 0) {
+    dim3 grid((unsigned)((long)B * wg.nWin), (unsigned)heads);
+    window_attention_kernel<<<grid, 256, 0, s>>>(QKV, relbias, RowOut{O, Oh, Ol}, C, wg);
+  } else {
+    const long npairs = (long)B * wg.nWin * heads;
+    const unsigned blocks = (unsigned)((npairs + 3) / 4);
+    if (passes == 3)
+      window_attention_mfma_kernel<3><<<blocks, 256, 0, s>>>(QKV, relmask, RowOut{O, Oh, Ol}, C, heads, npairs, wg);
+    else if (passes == 1)
+      window_attention_mfma_kernel<1><<<blocks, 256, 0, s>>>(QKV, relmask, RowOut{O, Oh, Ol}, C, heads, npairs, wg);
+    else
+      throw std::runtime_error("window_attention: passes must be 0, 1 or 3");
+  }
   MOCR_HIP_CHECK(hipGetLastError());
 }
 
