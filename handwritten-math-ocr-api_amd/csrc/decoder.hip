@@ -349,6 +349,379 @@ __global__ void __launch_bounds__(256) dec_attn_kernel(const DecodeState* st, in
   }
 }
 
+// ------------------------------------------------------------------ projection + attention
+// One workgroup per (row b, head h) does the head's q projection (self-attention: q, k
+// and v) from the LayerNorm'd input row and then attends, so the projection needs no
+// kernel of its own.  The cached K/V loads are issued first (they do not depend on this
+// step); the input row is normalised once per workgroup into LDS (one element per
+// thread, statistics merged by row_stats_16lanes: bit-identical to every other
+// consumer of that LayerNorm); thread (o = tid/8, kc = tid%8) dots output o's weight
+// row with k = 32kc..32kc+31, reduced over the 8 lanes in a fixed order.  The new
+// position's k/v (self-attention) enter the score loop from LDS and are appended to the
+// cache at t.  Attention: 8 lanes per key row, online softmax per wave, one barrier,
+// wave partials merged as in dec_attn_kernel.
+template <bool SELF, int NIT>
+__global__ void __launch_bounds__(256, 3) dec_projattn_kernel(ProjAttnParams p) {
+  constexpr int LPR = 8;  // lanes per key row (32 dims, float4 each)
+  constexpr int RPW = 8;  // key rows per wave instruction
+  constexpr int NP = SELF ? 3 : 1;
+  constexpr int CH = NIT < 4 ? NIT : 4;  // key groups (of 32) held in registers at a time
+  constexpr int NCH = (NIT + CH - 1) / CH;
+  __shared__ float xs[kD];
+  __shared__ float proj[NP][32];
+  __shared__ floatx4 po[4][LPR];
+  __shared__ float pm[4], ps[4];
+
+  const int b = blockIdx.x;
+  const int h = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int rsub = lane / LPR;
+  const int li = lane % LPR;
+  const int c4 = li * 4;
+  const int t = p.t;
+  const int n = p.n_cached + (SELF ? 1 : 0);
+  const int m_first = wave * RPW + rsub;
+
+  // key m of this row lives in K/V row slot_rows[b][m] (beam search: the hypothesis'
+  // ancestor that computed position m), else row b / mem_div (beams share their image's
+  // memory; 1 for greedy)
+  const float* Kh = p.K + h * 32 + c4;
+  const float* Vh = p.V + h * 32 + c4;
+  const int32_t* slots = p.slot_rows ? p.slot_rows + (size_t)b * p.slot_ld : nullptr;
+  const size_t fixed_row = (size_t)(b / p.mem_div);
+  floatx4 kk[CH], vv[CH];
+  auto load_chunk = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int it = c * CH + j;
+      const int m = m_first + it * 4 * RPW;
+      if (it < NIT && m < p.n_cached) {
+        const size_t r = slots ? (size_t)slots[m] : fixed_row;
+        kk[j] = *reinterpret_cast<const floatx4*>(Kh + r * p.kv_b_stride + (size_t)m * p.kv_row_stride);
+        vv[j] = *reinterpret_cast<const floatx4*>(Vh + r * p.kv_b_stride + (size_t)m * p.kv_row_stride);
+      } else {
+        kk[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        vv[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+  load_chunk(0);
+  // weight rows of this head's projections (independent of the input row)
+  const int o = tid >> 3;
+  const int kc = tid & 7;
+  floatx4 w[NP][8];
+#pragma unroll
+  for (int pj = 0; pj < NP; ++pj) {
+    const float* wr = p.W + (size_t)(pj * kD + h * 32 + o) * kD + 32 * kc;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[pj][i] = *reinterpret_cast<const floatx4*>(wr + 4 * i);
+  }
+  float xv = p.A[(size_t)b * kD + tid];
+  if (p.a_stats) {
+    const float g = p.a_ln_g[tid], be = p.a_ln_b[tid];
+    float mean, rstd;
+    row_stats_16lanes(p.a_stats + (size_t)b * 2 * kSlices, lane & 15, mean, rstd);
+    xv = ln_apply(xv, mean, rstd, g, be);
+  }
+  xs[tid] = xv;
+  __syncthreads();
+  float acc[NP];
+#pragma unroll
+  for (int pj = 0; pj < NP; ++pj) acc[pj] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const floatx4 x4 = *reinterpret_cast<const floatx4*>(&xs[32 * kc + 4 * i]);
+#pragma unroll
+    for (int pj = 0; pj < NP; ++pj)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[pj] = fmaf(x4[e], w[pj][i][e], acc[pj]);
+  }
+#pragma unroll
+  for (int pj = 0; pj < NP; ++pj) {
+    float a = acc[pj];
+    a += __shfl_xor(a, 1, 64);
+    a += __shfl_xor(a, 2, 64);
+    a += __shfl_xor(a, 4, 64);
+    if (kc == 0) proj[pj][o] = a + p.bias[pj * kD + h * 32 + o];
+  }
+  __syncthreads();
+  const floatx4 q4 = *reinterpret_cast<const floatx4*>(&proj[0][c4]);
+  floatx4 kn{}, vn{};
+  if constexpr (SELF) {
+    kn = *reinterpret_cast<const floatx4*>(&proj[1][c4]);
+    vn = *reinterpret_cast<const floatx4*>(&proj[2][c4]);
+    if (tid < 64 && !dec_skip(p.st, t)) {
+      float* dst = (tid < 32 ? p.kcache : p.vcache) + ((size_t)b * p.max_pos + t) * kD + h * 32 + (tid & 31);
+      *dst = proj[1 + (tid >> 5)][tid & 31];
+    }
+  }
+
+  // online softmax over chunks of CH key groups with a wave-uniform running max (one
+  // chunk: exactly the single-pass max / exp / sum)
+  float mrun = -INFINITY, sum = 0.f;
+  floatx4 o4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    if (c > 0) load_chunk(c);
+    if constexpr (SELF) {
+#pragma unroll
+      for (int j = 0; j < CH; ++j)
+        if (m_first + (c * CH + j) * 4 * RPW == t) {
+          kk[j] = kn;
+          vv[j] = vn;
+        }
+    }
+    float sc[CH];
+    float mc = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      float sv = q4[0] * kk[j][0];
+      sv = fmaf(q4[1], kk[j][1], sv);
+      sv = fmaf(q4[2], kk[j][2], sv);
+      sv = fmaf(q4[3], kk[j][3], sv);
+      sv += __shfl_xor(sv, 1, 64);
+      sv += __shfl_xor(sv, 2, 64);
+      sv += __shfl_xor(sv, 4, 64);
+      sv *= kAttnScale;
+      const int it = c * CH + j;
+      sc[j] = (it < NIT && m_first + it * 4 * RPW < n) ? sv : -INFINITY;
+      mc = fmaxf(mc, sc[j]);
+    }
+#pragma unroll
+    for (int off = LPR; off < 64; off <<= 1) mc = fmaxf(mc, __shfl_xor(mc, off, 64));
+    const float mnew = fmaxf(mrun, mc);
+    if (mnew != -INFINITY) {
+      const float scale = expf(mrun - mnew);
+      sum *= scale;
+      o4[0] *= scale;
+      o4[1] *= scale;
+      o4[2] *= scale;
+      o4[3] *= scale;
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        const float e = expf(sc[j] - mnew);
+        sum += e;
+        o4[0] = fmaf(e, vv[j][0], o4[0]);
+        o4[1] = fmaf(e, vv[j][1], o4[1]);
+        o4[2] = fmaf(e, vv[j][2], o4[2]);
+        o4[3] = fmaf(e, vv[j][3], o4[3]);
+      }
+      mrun = mnew;
+    }
+  }
+#pragma unroll
+  for (int off = LPR; off < 64; off <<= 1) {
+    sum += __shfl_xor(sum, off, 64);
+    o4[0] += __shfl_xor(o4[0], off, 64);
+    o4[1] += __shfl_xor(o4[1], off, 64);
+    o4[2] += __shfl_xor(o4[2], off, 64);
+    o4[3] += __shfl_xor(o4[3], off, 64);
+  }
+  if (rsub == 0) {
+    po[wave][li] = o4;
+    if (li == 0) {
+      pm[wave] = mrun;
+      ps[wave] = sum;
+    }
+  }
+  __syncthreads();
+  if (tid < 32 && !dec_skip(p.st, t)) {
+    float m = pm[0];
+#pragma unroll
+    for (int wv = 1; wv < 4; ++wv) m = fmaxf(m, pm[wv]);
+    float num = 0.f, den = 0.f;
+#pragma unroll
+    for (int wv = 0; wv < 4; ++wv) {
+      const float f = pm[wv] == -INFINITY ? 0.f : expf(pm[wv] - m);
+      num = fmaf(po[wv][tid / 4][tid % 4], f, num);
+      den = fmaf(ps[wv], f, den);
+    }
+    p.out[(size_t)b * kD + h * 32 + tid] = num / den;
+  }
+}
+
+// ------------------------------------------------------------------ beam search
+// Semantics: oracle/model_ref.py beam_search (the reference has none).
+// Row r = b*K + k is hypothesis k of image b, kept in rank order.
+__global__ void __launch_bounds__(256) beam_init_kernel(BeamParams p) {
+  const int r = blockIdx.x;
+  for (int c = threadIdx.x; c < p.d; c += blockDim.x)
+    p.x[(size_t)r * p.d + c] = p.emb[(size_t)p.sos * p.d + c] + p.pos[c];
+  if (threadIdx.x == 0) {
+    p.score[r] = (r % p.K == 0) ? 0.f : -INFINITY;
+    p.fin[r] = 0;
+    p.seq_new[(size_t)r * p.ld] = p.sos;  // buffer of parity 0
+  }
+}
+
+// (score, flat index) total order of the candidates: higher score, then lower index
+__device__ __forceinline__ bool cand_before(float s1, int f1, float s2, int f2) {
+  return s1 > s2 || (s1 == s2 && f1 < f2);
+}
+
+// sorted top-K lists with compile-time indices only (runtime-indexed arrays go to scratch)
+template <int K>
+__device__ __forceinline__ void topk_insert(float (&s)[K], int (&f)[K], float sv, int fv) {
+  if (!cand_before(sv, fv, s[K - 1], f[K - 1])) return;
+  s[K - 1] = sv;
+  f[K - 1] = fv;
+#pragma unroll
+  for (int j = K - 1; j > 0; --j) {
+    if (cand_before(s[j], f[j], s[j - 1], f[j - 1])) {
+      const float ts = s[j];
+      s[j] = s[j - 1];
+      s[j - 1] = ts;
+      const int tf = f[j];
+      f[j] = f[j - 1];
+      f[j - 1] = tf;
+    }
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void topk_merge(float (&s)[K], int (&f)[K], const float (&so)[K], const int (&fo)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) topk_insert<K>(s, f, so[k], fo[k]);
+}
+
+// One workgroup per image: log_softmax of the K beam rows (max, log Σ exp(l - max), as
+// torch.log_softmax), the K best of the K*V candidates, then the new beam: scores,
+// finished flags, token sequences and slot tables (double-buffered by step parity), and
+// the embedding of each new hypothesis' last token at position t+1.
+template <int K>
+__global__ void __launch_bounds__(256) beam_select_kernel(BeamParams p) {
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int t = p.t;
+  const int V = p.V;
+  __shared__ float s_max[K], s_lse[K];
+  __shared__ float ms[4][K];
+  __shared__ int mf[4][K];
+  __shared__ int s_par[K], s_tok[K];
+  __shared__ float s_sc[K];
+  __shared__ int s_fin[K];
+
+  // 1. per-beam max and log Σ exp(l - max)
+  for (int k = wave; k < K; k += 4) {
+    const float* L = p.logits + (size_t)(b * K + k) * p.ldl;
+    float m = -INFINITY, sm = 0.f;
+    for (int v = lane; v < V; v += 64) {
+      const float x = L[v];
+      if (x > m) {
+        sm = sm * expf(m - x) + 1.f;
+        m = x;
+      } else {
+        sm += expf(x - m);
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const float mo = __shfl_xor(m, off, 64);
+      const float so = __shfl_xor(sm, off, 64);
+      const float mm = fmaxf(m, mo);
+      sm = (m == -INFINITY ? 0.f : sm * expf(m - mm)) + (mo == -INFINITY ? 0.f : so * expf(mo - mm));
+      m = mm;
+    }
+    if (lane == 0) {
+      s_max[k] = m;
+      s_lse[k] = logf(sm);
+    }
+  }
+  __syncthreads();
+  // 2. candidates: live beam k offers score_k + logp_k[v]; a finished one, itself at k*V
+  float ts[K];
+  int tf[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    ts[k] = -INFINITY;
+    tf[k] = 0x7fffffff;
+  }
+  for (int k = 0; k < K; ++k) {
+    const int r = b * K + k;
+    const float sc = p.score[r];
+    const float* L = p.logits + (size_t)r * p.ldl;
+    if (p.fin[r]) {
+      if (tid == 0) topk_insert<K>(ts, tf, sc, k * V);
+    } else {
+      const float mk = s_max[k], lk = s_lse[k];
+      for (int v = tid; v < V; v += 256) topk_insert<K>(ts, tf, sc + ((L[v] - mk) - lk), k * V + v);
+    }
+  }
+  // 3. merge: 64 lanes by shuffles, then the 4 waves
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    float so[K];
+    int fo[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      so[k] = __shfl_xor(ts[k], off, 64);
+      fo[k] = __shfl_xor(tf[k], off, 64);
+    }
+    topk_merge<K>(ts, tf, so, fo);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      ms[wave][k] = ts[k];
+      mf[wave][k] = tf[k];
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 4; ++w) {
+      float so[K];
+      int fo[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        so[k] = ms[w][k];
+        fo[k] = mf[w][k];
+      }
+      topk_merge<K>(ts, tf, so, fo);
+    }
+    int all_fin = 1;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int parent = tf[k] / V;
+      const int pr = b * K + parent;
+      const int pfin = p.fin[pr];
+      const int tok = pfin ? p.pad : tf[k] - parent * V;
+      s_par[k] = pr;
+      s_tok[k] = tok;
+      s_sc[k] = ts[k];
+      s_fin[k] = pfin || tok == p.eos;
+      all_fin &= s_fin[k];
+    }
+    if (all_fin && p.stop_batch && !dec_skip(p.st, t)) {
+      const int before = atomicAdd(&p.st->nfinished, 1);
+      if (before == p.B - 1) p.st->done_step = t;
+    }
+  }
+  __syncthreads();
+  if (dec_skip(p.stop_batch ? p.st : nullptr, t)) return;
+  // 4. the new beam (every read of the old beam of this image happened before the barrier)
+  if (tid < K) {
+    p.score[b * K + tid] = s_sc[tid];
+    p.fin[b * K + tid] = s_fin[tid];
+  }
+  for (int i = tid; i < K * (t + 2); i += 256) {
+    const int k = i / (t + 2), j = i - k * (t + 2);
+    const size_t dst = (size_t)(b * K + k) * p.ld + j;
+    p.seq_new[dst] = j <= t ? p.seq_old[(size_t)s_par[k] * p.ld + j] : s_tok[k];
+    if (j < t) p.slot_new[dst] = p.slot_old[(size_t)s_par[k] * p.ld + j];
+    else if (j == t) p.slot_new[dst] = s_par[k];
+  }
+  if (!p.last_step) {
+    for (int i = tid; i < K * p.d; i += 256) {
+      const int k = i / p.d, c = i - k * p.d;
+      p.x[(size_t)(b * K + k) * p.d + c] = p.emb[(size_t)s_tok[k] * p.d + c] + p.pos[(size_t)(t + 1) * p.d + c];
+    }
+  }
+}
+
 // ------------------------------------------------------------------ greedy select
 // argmax over the vocabulary (first maximal index, as torch.argmax), log-prob of the
 // chosen token log(softmax + 1e-10) (app/src/im2latex.py:33-39), EOS bookkeeping for
@@ -495,6 +868,48 @@ void launch_dec_argmax(DecodeState* st, int t, int last_step, const float* logit
                        int d, hipStream_t s) {
   dec_argmax_kernel<<<B, 256, 0, s>>>(st, t, last_step, logits, hist_stride, ldl, V, ids, feed, forced, ld_ids, logp,
                                       finished, eos, stop_batch, emb, pos, x, d);
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+
+void launch_dec_projattn(const ProjAttnParams& p, bool self_attn, int n_max, hipStream_t s) {
+  if (p.d != kD || p.heads * 32 != kD) throw std::runtime_error("projattn: d_model 256, 8 heads of 32");
+  const int nit = (n_max + 31) / 32;
+  const dim3 grid(p.B, p.heads);
+#define MOCR_PA(N)                                                                        \
+  case N:                                                                                 \
+    if (self_attn)                                                                        \
+      dec_projattn_kernel<true, N><<<grid, 256, 0, s>>>(p);                               \
+    else                                                                                  \
+      dec_projattn_kernel<false, N><<<grid, 256, 0, s>>>(p);                              \
+    break;
+  if (p.mem_div < 1) throw std::runtime_error("projattn: mem_div must be >= 1");
+  switch (nit) {
+    MOCR_PA(1) MOCR_PA(2) MOCR_PA(3) MOCR_PA(4) MOCR_PA(5) MOCR_PA(6) MOCR_PA(7) MOCR_PA(8) MOCR_PA(9)
+    default: throw std::runtime_error("projattn: at most 288 keys");
+  }
+#undef MOCR_PA
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+
+void launch_beam_init(const BeamParams& p, hipStream_t s) {
+  beam_init_kernel<<<p.B * p.K, 256, 0, s>>>(p);
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_beam_select(const BeamParams& p, hipStream_t s) {
+  switch (p.K) {
+    case 1: beam_select_kernel<1><<<p.B, 256, 0, s>>>(p); break;
+    case 2: beam_select_kernel<2><<<p.B, 256, 0, s>>>(p); break;
+    case 3: beam_select_kernel<3><<<p.B, 256, 0, s>>>(p); break;
+    case 4: beam_select_kernel<4><<<p.B, 256, 0, s>>>(p); break;
+    case 5: beam_select_kernel<5><<<p.B, 256, 0, s>>>(p); break;
+    case 6: beam_select_kernel<6><<<p.B, 256, 0, s>>>(p); break;
+    case 7: beam_select_kernel<7><<<p.B, 256, 0, s>>>(p); break;
+    case 8: beam_select_kernel<8><<<p.B, 256, 0, s>>>(p); break;
+    default: throw std::runtime_error("beam: 1..8 hypotheses per image");
+  }
   MOCR_HIP_CHECK(hipGetLastError());
 }
 

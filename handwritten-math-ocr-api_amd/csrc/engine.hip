@@ -11,6 +11,8 @@
 #include <vector>
 
 #include "../../include/mathocr.h"
+#include <cstdlib>
+
 #include "kernels.h"
 
 using namespace mocr;
@@ -131,7 +133,8 @@ void check_config(const mocr_config& c) {
   req(c.d_model == 256 && c.n_heads == 8, "decoder kernels are built for d_model=256, 8 heads");
   req(c.d_ff == 512, "decoder kernels are built for d_ff=512");
   req(c.n_layers >= 1 && c.n_layers <= 64, "n_layers");
-  req(c.max_pos >= 2 && c.max_pos <= 256, "max_pos in [2,256]");
+  req(c.max_pos >= 2 && c.max_pos <= 288, "max_pos in [2,288]");
+  req(c.max_beam >= 0 && c.max_beam <= 8, "max_beam in [0,8]");
   req(c.max_batch >= 1 && c.max_batch <= 4096, "max_batch");
   req(c.precision == MOCR_PRECISION_FP32 || c.precision == MOCR_PRECISION_BF16 ||
           c.precision == MOCR_PRECISION_BF16X3,
@@ -218,6 +221,12 @@ struct mocr_engine {
   float* logp = nullptr;
   DecodeState* st = nullptr;
   int ld_ids = 0;
+  int max_rows = 0;  // decoder rows the buffers hold: max_batch * max(1, max_beam)
+  // beam search: scores, finished flags, token sequences and K/V slot tables [2 parities]
+  float* bscore = nullptr;
+  int32_t* bfin = nullptr;
+  int32_t* bseq[2] = {nullptr, nullptr};
+  int32_t* bslot[2] = {nullptr, nullptr};
   std::map<std::tuple<int, int, int>, hipGraphExec_t> graphs;
 
   // timing
@@ -238,7 +247,8 @@ struct mocr_engine {
                     ATT,     HID,     MEM,     MEMKV,   dx,      dq,   datt,     dy_sa,    dy_ca,  dy_ff, dh, dlogits,
                     ds_sa,   ds_ca,   ds_ff,
                     dlogits_hist, kcache, vcache, ids, feed, forced, finished, logp, st, XWh, XWl, ATTh, ATTl,
-                    HIDh, HIDl, MEMh, MEMl, dwh, dwl, kvwh, kvwl};
+                    HIDh, HIDl, MEMh, MEMl, dwh, dwl, kvwh, kvwl, bscore, bfin, bseq[0], bseq[1],
+                    bslot[0], bslot[1]};
     for (void* p : bufs)
       if (p) (void)hipFree(p);
     for (float* p : relbias)
@@ -325,20 +335,31 @@ struct mocr_engine {
       }
     }
 
-    dx = dalloc<float>(B * d);
-    dq = dalloc<float>(B * d);
-    datt = dalloc<float>(B * d);
-    dy_sa = dalloc<float>(B * d);
-    dy_ca = dalloc<float>(B * d);
-    dy_ff = dalloc<float>(B * d);
-    ds_sa = dalloc<float>(B * 32);
-    ds_ca = dalloc<float>(B * 32);
-    ds_ff = dalloc<float>(B * 32);
-    dh = dalloc<float>(B * cfg.d_ff);
-    dlogits = dalloc<float>(B * Vpad);
-    kcache = dalloc<float>(L * B * cfg.max_pos * d);
-    vcache = dalloc<float>(L * B * cfg.max_pos * d);
+    // decoder rows: one per image (greedy) or per hypothesis (beam search)
+    const size_t R = B * std::max(1, cfg.max_beam);
+    max_rows = (int)R;
+    dx = dalloc<float>(R * d);
+    dq = dalloc<float>(R * d);
+    datt = dalloc<float>(R * d);
+    dy_sa = dalloc<float>(R * d);
+    dy_ca = dalloc<float>(R * d);
+    dy_ff = dalloc<float>(R * d);
+    ds_sa = dalloc<float>(R * 32);
+    ds_ca = dalloc<float>(R * 32);
+    ds_ff = dalloc<float>(R * 32);
+    dh = dalloc<float>(R * cfg.d_ff);
+    dlogits = dalloc<float>(R * Vpad);
+    kcache = dalloc<float>(L * R * cfg.max_pos * d);
+    vcache = dalloc<float>(L * R * cfg.max_pos * d);
     ld_ids = cfg.max_pos + 1;
+    if (cfg.max_beam > 0) {
+      bscore = dalloc<float>(R);
+      bfin = dalloc<int32_t>(R);
+      for (int i = 0; i < 2; ++i) {
+        bseq[i] = dalloc<int32_t>(R * ld_ids);
+        bslot[i] = dalloc<int32_t>(R * ld_ids);
+      }
+    }
     ids = dalloc<int32_t>(B * ld_ids);
     feed = dalloc<int32_t>(B * ld_ids);
     forced = dalloc<int32_t>(B * ld_ids);
@@ -485,6 +506,8 @@ struct mocr_engine {
   };
   Operand wop(size_t off) const { return {dw + off, dwh ? dwh + off : nullptr, dwl ? dwl + off : nullptr}; }
   bool bf16_mode() const { return cfg.precision != MOCR_PRECISION_FP32; }
+  // decoder: head projections fused into the attention kernels (MOCR_DEC_FUSED=0: separate)
+  const bool fused_attn = getenv("MOCR_DEC_FUSED") == nullptr || atoi(getenv("MOCR_DEC_FUSED")) != 0;
   int attn_passes() const {
     return cfg.precision == MOCR_PRECISION_FP32 ? 0 : (cfg.precision == MOCR_PRECISION_BF16X3 ? 3 : 1);
   }
@@ -625,11 +648,12 @@ struct mocr_engine {
   // One greedy step t.  Buffers: dx = fed-token embedding (layer-0 input),
   // ysa/yca/yff = pre-LayerNorm sums of the three post-norm sublayers; LN1/LN2/LN3 are
   // applied by their consumers.  stp = stop state (nullptr unless batch-global stop).
-  void record_step(int B, int t, int max_steps, bool hist, bool use_forced, bool stop_batch) {
+  // The decoder layers of step t over `B` decoder rows (images, or hypotheses with beam
+  // search: self-attention keys through `slots`, memory row = row / mem_div).
+  void record_layers(int B, int t, const DecodeState* stp, const int32_t* slots, int mem_div) {
     const int d = cfg.d_model, L = cfg.n_layers;
-    const size_t cache_layer = (size_t)cfg.max_batch * cfg.max_pos * d;
+    const size_t cache_layer = (size_t)max_rows * cfg.max_pos * d;
     const size_t kv_layer = (size_t)cfg.max_batch * M * 2 * d;
-    const DecodeState* stp = stop_batch ? st : nullptr;
     hipStream_t s = stream;
     auto base = [&]() {
       RowGemmParams p{};
@@ -639,6 +663,18 @@ struct mocr_engine {
       p.d = d;
       p.max_pos = cfg.max_pos;
       return p;
+    };
+    auto pa_base = [&]() {
+      ProjAttnParams a{};
+      a.st = stp;
+      a.t = t;
+      a.out = datt;
+      a.B = B;
+      a.d = d;
+      a.heads = cfg.n_heads;
+      a.max_pos = cfg.max_pos;
+      a.mem_div = 1;
+      return a;
     };
     for (int l = 0; l < L; ++l) {
       const DecLayerW& w = lay->layers[l];
@@ -652,24 +688,40 @@ struct mocr_engine {
       const float* xin_s = l ? ds_ff : nullptr;
       // self-attention block: y_sa = x + SA(x)
       RowGemmParams p = base();
-      p.A = xin; p.a_ln_g = xin_g; p.a_ln_b = xin_b; p.a_stats = xin_s; p.W = W(w.sa_inw); p.bias = W(w.sa_inb);
-      p.out = dq; p.kcache = kc; p.vcache = vc; p.N = 3 * d; p.K = d; p.ldo = d; p.n_valid = 3 * d;
-      p.epi = DEC_QKV;
-      launch_rowgemm(p, s);
-      launch_dec_attn(stp, t, dq, kc, vc, (size_t)cfg.max_pos * d, d, t + 1, t + 1, datt, B, d, cfg.n_heads, s);
+      if (fused_attn) {
+        ProjAttnParams a = pa_base();
+        a.A = xin; a.a_ln_g = xin_g; a.a_ln_b = xin_b; a.a_stats = xin_s; a.W = W(w.sa_inw); a.bias = W(w.sa_inb);
+        a.K = kc; a.V = vc; a.kv_b_stride = (size_t)cfg.max_pos * d; a.kv_row_stride = d; a.n_cached = t;
+        a.kcache = kc; a.vcache = vc; a.slot_rows = slots; a.slot_ld = ld_ids;
+        launch_dec_projattn(a, true, t + 1, s);
+      } else {
+        p.A = xin; p.a_ln_g = xin_g; p.a_ln_b = xin_b; p.a_stats = xin_s; p.W = W(w.sa_inw); p.bias = W(w.sa_inb);
+        p.out = dq; p.kcache = kc; p.vcache = vc; p.N = 3 * d; p.K = d; p.ldo = d; p.n_valid = 3 * d;
+        p.epi = DEC_QKV;
+        launch_rowgemm(p, s);
+        launch_dec_attn(stp, t, dq, kc, vc, (size_t)cfg.max_pos * d, d, t + 1, t + 1, datt, B, d, cfg.n_heads, s);
+      }
       p = base();
       p.A = datt; p.W = W(w.sa_ow); p.bias = W(w.sa_ob); p.out = dy_sa; p.resid = xin; p.r_ln_g = xin_g;
       p.r_ln_b = xin_b; p.r_stats = xin_s; p.out_stats = ds_sa; p.N = d; p.K = d; p.ldo = d; p.n_valid = d;
       p.epi = DEC_RESADD;
       launch_rowgemm(p, s);
       // cross-attention block: y_ca = LN1(y_sa) + MHA(LN1(y_sa), mem)
-      p = base();
-      p.A = dy_sa; p.a_ln_g = W(w.n1w); p.a_ln_b = W(w.n1b); p.a_stats = ds_sa; p.W = W(w.ca_inw);
-      p.bias = W(w.ca_inb);
-      p.out = dq; p.N = d; p.K = d; p.ldo = d; p.n_valid = d; p.epi = DEC_STORE;
-      launch_rowgemm(p, s);
       const float* memk = MEMKV + l * kv_layer;
-      launch_dec_attn(stp, t, dq, memk, memk + d, (size_t)M * 2 * d, 2 * d, M, M, datt, B, d, cfg.n_heads, s);
+      if (fused_attn) {
+        ProjAttnParams a = pa_base();
+        a.A = dy_sa; a.a_ln_g = W(w.n1w); a.a_ln_b = W(w.n1b); a.a_stats = ds_sa; a.W = W(w.ca_inw);
+        a.bias = W(w.ca_inb); a.K = memk; a.V = memk + d; a.kv_b_stride = (size_t)M * 2 * d; a.kv_row_stride = 2 * d;
+        a.n_cached = M; a.mem_div = mem_div;
+        launch_dec_projattn(a, false, M, s);
+      } else {
+        p = base();
+        p.A = dy_sa; p.a_ln_g = W(w.n1w); p.a_ln_b = W(w.n1b); p.a_stats = ds_sa; p.W = W(w.ca_inw);
+        p.bias = W(w.ca_inb);
+        p.out = dq; p.N = d; p.K = d; p.ldo = d; p.n_valid = d; p.epi = DEC_STORE;
+        launch_rowgemm(p, s);
+        launch_dec_attn(stp, t, dq, memk, memk + d, (size_t)M * 2 * d, 2 * d, M, M, datt, B, d, cfg.n_heads, s);
+      }
       p = base();
       p.A = datt; p.W = W(w.ca_ow); p.bias = W(w.ca_ob); p.out = dy_ca; p.resid = dy_sa; p.r_ln_g = W(w.n1w);
       p.r_ln_b = W(w.n1b); p.r_stats = ds_sa; p.out_stats = ds_ca; p.N = d; p.K = d; p.ldo = d; p.n_valid = d;
@@ -687,40 +739,101 @@ struct mocr_engine {
       p.n_valid = d; p.epi = DEC_RESADD;
       launch_rowgemm(p, s);
     }
+  }
+
+  // Logits of the last layer's LN3 output over `B` rows into `out` (row stride Vpad).
+  void record_logits(int B, int t, const DecodeState* stp, float* out, size_t hist_stride) {
+    const int d = cfg.d_model, L = cfg.n_layers;
     const DecLayerW& last = lay->layers[L - 1];
-    RowGemmParams p = base();
+    RowGemmParams p{};
+    p.B = B;
+    p.st = stp;
+    p.t = t;
+    p.d = d;
+    p.max_pos = cfg.max_pos;
     p.A = dy_ff;
     p.a_ln_g = W(last.n3w);
     p.a_ln_b = W(last.n3b);
     p.a_stats = ds_ff;
     p.W = fcw_pad;
     p.bias = fcb_pad;
-    p.out = hist ? dlogits_hist : dlogits;
-    p.hist_stride = hist ? (size_t)cfg.max_batch * Vpad : 0;
+    p.out = out;
+    p.hist_stride = hist_stride;
     p.N = Vpad;
     p.K = d;
     p.ldo = Vpad;
     p.n_valid = cfg.vocab;
     p.epi = DEC_LOGITS;
-    launch_rowgemm(p, s);
-    launch_dec_argmax(st, t, t + 1 >= max_steps, p.out, p.hist_stride, Vpad, cfg.vocab, B, ids, feed,
-                      use_forced ? forced : nullptr, ld_ids, logp, finished, cfg.eos_id, stop_batch ? 1 : 0,
-                      W(lay->emb), W(lay->pos), dx, d, s);
+    launch_rowgemm(p, stream);
   }
 
+  void record_step(int B, int t, int max_steps, bool hist, bool use_forced, bool stop_batch) {
+    const DecodeState* stp = stop_batch ? st : nullptr;
+    record_layers(B, t, stp, nullptr, 1);
+    float* out = hist ? dlogits_hist : dlogits;
+    const size_t hs = hist ? (size_t)cfg.max_batch * Vpad : 0;
+    record_logits(B, t, stp, out, hs);
+    launch_dec_argmax(st, t, t + 1 >= max_steps, out, hs, Vpad, cfg.vocab, B, ids, feed, use_forced ? forced : nullptr,
+                      ld_ids, logp, finished, cfg.eos_id, stop_batch ? 1 : 0, W(lay->emb), W(lay->pos), dx,
+                      cfg.d_model, stream);
+  }
+
+  BeamParams beam_params(int B, int K, int t, int max_steps, bool stop_batch) {
+    BeamParams b{};
+    b.st = st;
+    b.t = t;
+    b.last_step = t + 1 >= max_steps;
+    b.stop_batch = stop_batch;
+    b.B = B;
+    b.K = K;
+    b.V = cfg.vocab;
+    b.ldl = Vpad;
+    b.d = cfg.d_model;
+    b.ld = ld_ids;
+    b.sos = cfg.sos_id;
+    b.eos = cfg.eos_id;
+    b.pad = cfg.pad_id;
+    b.logits = dlogits;
+    b.score = bscore;
+    b.fin = bfin;
+    b.seq_old = bseq[t & 1];
+    b.seq_new = bseq[(t + 1) & 1];
+    b.slot_old = bslot[t & 1];
+    b.slot_new = bslot[(t + 1) & 1];
+    b.emb = W(lay->emb);
+    b.pos = W(lay->pos);
+    b.x = dx;
+    return b;
+  }
+
+  // One beam-search step over B images x K hypotheses (oracle/model_ref.py beam_search).
+  void record_beam_step(int B, int K, int t, int max_steps, bool stop_batch) {
+    const DecodeState* stp = stop_batch ? st : nullptr;
+    record_layers(B * K, t, stp, bslot[t & 1], K);
+    record_logits(B * K, t, stp, dlogits, 0);
+    launch_beam_select(beam_params(B, K, t, max_steps, stop_batch), stream);
+  }
+
+
   // Graph of steps [c*kDecodeChunk, min(max_steps, (c+1)*kDecodeChunk)), step indices baked in.
-  hipGraphExec_t graph_for(int B, int c, int max_steps, bool hist, bool use_forced, bool stop_batch) {
+  // beam > 0: beam-search steps with that many hypotheses per image.
+  hipGraphExec_t graph_for(int B, int c, int max_steps, bool hist, bool use_forced, bool stop_batch, int beam = 0) {
     const int t0 = c * kDecodeChunk;
     const int t1 = std::min(max_steps, t0 + kDecodeChunk);
     const bool ends = t1 == max_steps;  // the last step skips the next embedding
-    const int flags = (int)hist | (int)use_forced << 1 | (int)stop_batch << 2 | (int)ends << 3;
+    const int flags = (int)hist | (int)use_forced << 1 | (int)stop_batch << 2 | (int)ends << 3 | beam << 4;
     auto key = std::make_tuple(B, t0 * 1000 + t1, flags);
     auto it = graphs.find(key);
     if (it != graphs.end()) return it->second;
     hipGraph_t g;
     MOCR_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     try {
-      for (int t = t0; t < t1; ++t) record_step(B, t, max_steps, hist, use_forced, stop_batch);
+      for (int t = t0; t < t1; ++t) {
+        if (beam)
+          record_beam_step(B, beam, t, max_steps, stop_batch);
+        else
+          record_step(B, t, max_steps, hist, use_forced, stop_batch);
+      }
     } catch (...) {
       (void)hipStreamEndCapture(stream, &g);
       throw;
@@ -778,6 +891,54 @@ struct mocr_engine {
     MOCR_HIP_CHECK(hipStreamSynchronize(stream));
     return stop_batch && hs.done_step != 0x7fffffff ? hs.done_step + 1 : max_steps;
   }
+  void decode_beam_out(int K, int max_steps, int stop_mode, int32_t* ids_out, float* scores_out, int32_t* beam_ids_out,
+                       int32_t* n_steps_out) {
+    const int n = decode_beam(K, max_steps, stop_mode);
+    const int B = cur_batch, ld = ld_ids, Wd = max_steps + 1;
+    std::vector<int32_t> seq((size_t)B * K * ld);
+    std::vector<float> sc((size_t)B * K);
+    MOCR_HIP_CHECK(hipMemcpy(seq.data(), bseq[n & 1], seq.size() * 4, hipMemcpyDeviceToHost));
+    MOCR_HIP_CHECK(hipMemcpy(sc.data(), bscore, sc.size() * 4, hipMemcpyDeviceToHost));
+    for (int r = 0; r < B * K; ++r)
+      for (int j = 0; j < Wd; ++j) {
+        const int32_t v = j <= n ? seq[(size_t)r * ld + j] : cfg.pad_id;
+        if (beam_ids_out) beam_ids_out[(size_t)r * Wd + j] = v;
+        if (ids_out && r % K == 0) ids_out[(size_t)(r / K) * Wd + j] = v;  // rank 0 = best
+      }
+    if (scores_out) std::memcpy(scores_out, sc.data(), sc.size() * 4);
+    if (n_steps_out) *n_steps_out = n;
+  }
+
+  // Beam search over the encoded batch; returns the steps run.  Results stay in
+  // bseq[n & 1] (rank order) and bscore.
+  int decode_beam(int K, int max_steps, int stop_mode) {
+    if (!encoded) throw std::runtime_error("mocr_decode_beam before mocr_encode");
+    if (K < 1 || K > cfg.max_beam) throw std::runtime_error("beam must be in [1, max_beam]");
+    if (max_steps < 1 || max_steps > cfg.max_pos) throw std::runtime_error("max_steps must be in [1, max_pos]");
+    if (stop_mode != MOCR_STOP_BATCH && stop_mode != MOCR_STOP_NONE) throw std::runtime_error("bad stop_mode");
+    MOCR_HIP_CHECK(hipSetDevice(device));
+    const int B = cur_batch;
+    const bool stop_batch = stop_mode == MOCR_STOP_BATCH;
+    DecodeState h{};
+    h.done_step = 0x7fffffff;
+    h.batch = B;
+    MOCR_HIP_CHECK(hipMemcpyAsync(st, &h, sizeof(h), hipMemcpyHostToDevice, stream));
+    launch_beam_init(beam_params(B, K, -1, max_steps, stop_batch), stream);
+    const int chunks = (max_steps + kDecodeChunk - 1) / kDecodeChunk;
+    DecodeState hs{};
+    for (int c = 0; c < chunks; ++c) {
+      MOCR_HIP_CHECK(hipGraphLaunch(graph_for(B, c, max_steps, false, false, stop_batch, K), stream));
+      if (stop_batch && c + 1 < chunks) {
+        MOCR_HIP_CHECK(hipMemcpyAsync(&hs, st, sizeof(hs), hipMemcpyDeviceToHost, stream));
+        MOCR_HIP_CHECK(hipStreamSynchronize(stream));
+        if (hs.done_step != 0x7fffffff) break;
+      }
+    }
+    MOCR_HIP_CHECK(hipMemcpyAsync(&hs, st, sizeof(hs), hipMemcpyDeviceToHost, stream));
+    MOCR_HIP_CHECK(hipStreamSynchronize(stream));
+    return stop_batch && hs.done_step != 0x7fffffff ? hs.done_step + 1 : max_steps;
+  }
+
 
   void copy_ids(int32_t* dst, int max_steps, hipMemcpyKind kind) {
     MOCR_HIP_CHECK(hipMemcpy2DAsync(dst, (max_steps + 1) * 4, ids, ld_ids * 4, (max_steps + 1) * 4, cur_batch, kind,
@@ -872,6 +1033,11 @@ int mocr_get_memory(mocr_engine* eng, float* host_out) {
     MOCR_HIP_CHECK(hipMemcpy(host_out, eng->MEM, (size_t)eng->cur_batch * eng->M * eng->cfg.d_model * sizeof(float),
                              hipMemcpyDeviceToHost));
   })
+}
+
+int mocr_decode_beam(mocr_engine* eng, int beam, int max_steps, int stop_mode, int32_t* ids_out, float* scores_out,
+                     int32_t* beam_ids_out, int32_t* n_steps_out) {
+  MOCR_API_BODY(eng, eng->decode_beam_out(beam, max_steps, stop_mode, ids_out, scores_out, beam_ids_out, n_steps_out))
 }
 
 int mocr_decode(mocr_engine* eng, int max_steps, int stop_mode, const int32_t* forced_ids, int32_t* ids_out,

@@ -116,6 +116,56 @@ void launch_dec_embed0(const int32_t* feed, int ld_ids, const float* emb, const 
 
 // Attention of the newest position over n keys (self: n = t+1 from the KV cache;
 // cross: n = M memory tokens).  K/V rows for image b start at K + b*kv_b_stride.
+// Fused head projection + attention of the newest position (decoder.hip
+// dec_projattn_kernel), one workgroup per (row, head).  Self-attention: W/bias are the
+// in_proj [3d][d] rows (q, k, v); K/V = the layer's cache (kv_b_stride = max_pos*d,
+// row stride d), n_cached = t; the new k/v are appended at t.  Cross-attention: W/bias
+// the q rows of the in_proj, K/V = the precomputed memory K/V, n_cached = M.
+struct ProjAttnParams {
+  const DecodeState* st;
+  int t;
+  const float* A;        // [B, d] layer input (pre-norm sum)
+  const float* a_stats;  // its LayerNorm slice stats [B][16][2], or null (embedding input)
+  const float* a_ln_g;
+  const float* a_ln_b;
+  const float* W;
+  const float* bias;
+  const float* K;
+  const float* V;
+  size_t kv_b_stride;
+  int kv_row_stride;
+  int n_cached;
+  float* kcache;  // self-attention only
+  float* vcache;
+  float* out;     // [B, d]
+  int B, d, heads, max_pos;
+  const int32_t* slot_rows;  // beam self-attention: [B][slot_ld] K/V row of key m, or null
+  int slot_ld;
+  int mem_div;               // K/V row = b / mem_div when slot_rows is null (>= 1)
+};
+void launch_dec_projattn(const ProjAttnParams& p, bool self_attn, int n_max, hipStream_t s);
+
+// Beam search state and step kernels (decoder.hip; semantics oracle/model_ref.py
+// beam_search).  Rows r = b*K + k.
+struct BeamParams {
+  DecodeState* st;
+  int t, last_step, stop_batch;
+  int B, K, V, ldl, d, ld;  // ld = max_pos + 1 (sequence / slot table row stride)
+  int sos, eos, pad;
+  const float* logits;      // [B*K, ldl]
+  float* score;             // [B*K]
+  int32_t* fin;             // [B*K]
+  const int32_t* seq_old;   // [B*K, ld] token sequences, step parity t & 1
+  int32_t* seq_new;         // parity (t + 1) & 1
+  const int32_t* slot_old;  // [B*K, ld] K/V cache row of each position
+  int32_t* slot_new;
+  const float* emb;
+  const float* pos;
+  float* x;                 // [B*K, d] next step's input
+};
+void launch_beam_init(const BeamParams& p, hipStream_t s);
+void launch_beam_select(const BeamParams& p, hipStream_t s);
+
 void launch_dec_attn(const DecodeState* st, int t, const float* q, const float* K, const float* V,
                      size_t kv_b_stride, int kv_row_stride, int n_fixed, int n_max, float* out, int B, int d,
                      int heads, hipStream_t s);

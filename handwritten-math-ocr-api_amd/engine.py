@@ -22,12 +22,13 @@ LIB_PATH = os.path.join(_HERE, "lib", "libmathocr.so")
 
 PRECISION = {"fp32": 0, "bf16": 1, "bf16x3": 2}
 STOP = {"batch": 0, "none": 1}
+ABI_VERSION = 2
 
 
 class MocrConfig(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "img_h", "img_w", "vocab", "d_model", "n_heads", "d_ff", "n_layers", "max_pos",
-        "sos_id", "eos_id", "pad_id", "max_batch", "precision")]
+        "sos_id", "eos_id", "pad_id", "max_batch", "precision", "max_beam")]
 
 
 class KernelStat(ctypes.Structure):
@@ -64,6 +65,7 @@ def load_library(path: str = LIB_PATH):
         "mocr_get_memory": (I, [P, f32p]),
         "mocr_decode": (I, [P, I, I, i32p, i32p, i32p, f32p, f32p]),
         "mocr_decode_device": (I, [P, I, I, P, i32p]),
+        "mocr_decode_beam": (I, [P, I, I, I, i32p, f32p, i32p, i32p]),
         "mocr_debug_encode_until": (I, [P, I, I, f32p, SZ]),
         "mocr_set_timing": (I, [P, I]),
         "mocr_get_timing": (I, [P, ctypes.POINTER(KernelStat), I]),
@@ -72,7 +74,7 @@ def load_library(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.mocr_abi_version() != 1:
+    if lib.mocr_abi_version() != ABI_VERSION:
         raise RuntimeError("libmathocr.so ABI version mismatch")
     _lib = lib
     return lib
@@ -81,15 +83,15 @@ def load_library(path: str = LIB_PATH):
 def exported_symbols():
     return ["mocr_abi_version", "mocr_weight_count", "mocr_memory_tokens", "mocr_create", "mocr_destroy",
             "mocr_last_error", "mocr_load_weights", "mocr_set_images", "mocr_set_images_device", "mocr_encode",
-            "mocr_get_memory", "mocr_decode", "mocr_decode_device", "mocr_debug_encode_until", "mocr_set_timing",
-            "mocr_get_timing"]
+            "mocr_get_memory", "mocr_decode", "mocr_decode_device", "mocr_decode_beam", "mocr_debug_encode_until",
+            "mocr_set_timing", "mocr_get_timing"]
 
 
 def make_config(img_hw=(96, 320), vocab=synth.VOCAB, max_batch=64, precision="fp32", n_layers=synth.N_LAYERS,
-                max_pos=synth.MAX_POS, sos=synth.SOS_ID, eos=synth.EOS_ID, pad=synth.PAD_ID) -> MocrConfig:
+                max_pos=synth.MAX_POS, sos=synth.SOS_ID, eos=synth.EOS_ID, pad=synth.PAD_ID, max_beam=0) -> MocrConfig:
     return MocrConfig(img_h=img_hw[0], img_w=img_hw[1], vocab=vocab, d_model=synth.D_MODEL, n_heads=synth.N_HEADS,
                       d_ff=synth.D_FF, n_layers=n_layers, max_pos=max_pos, sos_id=sos, eos_id=eos, pad_id=pad,
-                      max_batch=max_batch, precision=PRECISION[precision])
+                      max_batch=max_batch, precision=PRECISION[precision], max_beam=max_beam)
 
 
 def _f32p(a):
@@ -98,6 +100,14 @@ def _f32p(a):
 
 def _i32p(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+
+
+@dataclass
+class BeamResult:
+    ids: np.ndarray        # [B, n_steps+1] int32 best hypothesis, column 0 = sos, pad after it ends
+    scores: np.ndarray     # [B, K] summed log-probs, rank order
+    beams: np.ndarray      # [B, K, n_steps+1] every hypothesis, rank order
+    n_steps: int
 
 
 @dataclass
@@ -117,9 +127,10 @@ class Engine:
 
     def __init__(self, img_hw=(96, 320), vocab=synth.VOCAB, max_batch=64, precision="fp32", device=0,
                  n_layers=synth.N_LAYERS, max_pos=synth.MAX_POS, sos=synth.SOS_ID, eos=synth.EOS_ID,
-                 pad=synth.PAD_ID):
+                 pad=synth.PAD_ID, max_beam=0):
         self.lib = load_library()
-        self.cfg = make_config(img_hw, vocab, max_batch, precision, n_layers, max_pos, sos, eos, pad)
+        self.cfg = make_config(img_hw, vocab, max_batch, precision, n_layers, max_pos, sos, eos, pad, max_beam)
+        self.max_beam = max_beam
         self.img_hw = tuple(img_hw)
         self.vocab = vocab
         self.max_batch = max_batch
@@ -228,6 +239,19 @@ class Engine:
         k = n.value
         return DecodeResult(ids[:, :k + 1], k, logp[:, :k] if logp is not None else None,
                             logits[:, :k] if logits is not None else None)
+
+    def beam_search(self, beam=4, max_steps=256, stop="batch") -> BeamResult:
+        """Beam search of the encoded batch (``mocr_decode_beam``; semantics:
+        oracle/model_ref.py ``beam_search``)."""
+        B = self.batch
+        W = max_steps + 1
+        beams = np.empty((B, beam, W), np.int32)
+        scores = np.empty((B, beam), np.float32)
+        n = ctypes.c_int32()
+        self._check(self.lib.mocr_decode_beam(self._h, beam, max_steps, STOP[stop], None, _f32p(scores),
+                                              _i32p(beams), ctypes.byref(n)), "mocr_decode_beam")
+        k = n.value
+        return BeamResult(ids=beams[:, 0, :k + 1].copy(), scores=scores, beams=beams[:, :, :k + 1].copy(), n_steps=k)
 
     def decode_into(self, ids_dev, max_steps=150, stop="batch") -> int:
         """Decode and write ids [B, max_steps+1] int32 into a device tensor (e.g. a torch

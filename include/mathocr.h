@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MOCR_ABI_VERSION 1
+#define MOCR_ABI_VERSION 2
 
 /* Arithmetic of the engine. */
 enum {
@@ -67,6 +67,7 @@ typedef struct mocr_config {
   int32_t sos_id, eos_id, pad_id; /* 1, 2, 0 (src/utils.py:111)                                    */
   int32_t max_batch;     /* device buffers are sized for this many images                          */
   int32_t precision;     /* MOCR_PRECISION_*                                                       */
+  int32_t max_beam;      /* 0: greedy only; K <= 8: decoder buffers for max_batch*K hypotheses      */
 } mocr_config;
 
 typedef struct mocr_engine mocr_engine;
@@ -112,6 +113,21 @@ int mocr_get_memory(mocr_engine* eng, float* host_out);
  *   logits_out  nullable [B, max_steps, vocab] fp32 last-position logits (parity only). */
 int mocr_decode(mocr_engine* eng, int max_steps, int stop_mode, const int32_t* forced_ids,
                 int32_t* ids_out, int32_t* n_steps_out, float* logp_out, float* logits_out);
+
+/* Beam search of the encoded batch.  The reference's beam_size
+ * argument (src/inference.py:7, src/config.py:50) is accepted but unused, so the
+ * semantics are this engine's, restated on the CPU by oracle/model_ref.py
+ * beam_search: K hypotheses per image in rank order, score = sum of log_softmax of
+ * the chosen tokens (no length penalty), finished hypotheses retained at unchanged
+ * score, ties broken by the lower (beam * V + token) index.
+ *   beam         1 <= K <= cfg.max_beam;
+ *   ids_out      nullable [B, max_steps+1]: the best hypothesis, column 0 = sos, pad after;
+ *   scores_out   nullable [B, K] hypothesis scores, rank order;
+ *   beam_ids_out nullable [B, K, max_steps+1] every hypothesis;
+ *   n_steps_out  steps run (< max_steps only with MOCR_STOP_BATCH: every hypothesis of
+ *                every image finished). */
+int mocr_decode_beam(mocr_engine* eng, int beam, int max_steps, int stop_mode, int32_t* ids_out, float* scores_out,
+                     int32_t* beam_ids_out, int32_t* n_steps_out);
 
 /* Same, ids written to caller device memory [B, max_steps+1] (e.g. a torch tensor
  * that is then all-gathered over RCCL). */

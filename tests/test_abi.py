@@ -22,7 +22,14 @@ def test_header_symbols_exported(pkg):
     for n in names:
         assert hasattr(lib, n), n
     assert sorted(pkg.engine.exported_symbols()) == names
-    assert lib.mocr_abi_version() == 1
+    header = open(os.path.join(os.path.dirname(__file__), "..", "include", "mathocr.h")).read()
+    version = int(re.search(r"#define MOCR_ABI_VERSION (\d+)", header).group(1))
+    assert lib.mocr_abi_version() == version == pkg.engine.ABI_VERSION
+    # the ctypes mirror of mocr_config has the header's fields, in order
+    body = re.search(r"typedef struct mocr_config \{(.*?)\} mocr_config;", header, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    fields = [f.strip() for decl in re.findall(r"int32_t([^;]*);", body) for f in decl.split(",")]
+    assert fields == [n for n, _ in pkg.engine.MocrConfig._fields_]
 
 
 def test_weight_count_matches_spec(pkg):
