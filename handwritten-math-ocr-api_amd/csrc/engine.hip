@@ -506,8 +506,12 @@ struct mocr_engine {
   };
   Operand wop(size_t off) const { return {dw + off, dwh ? dwh + off : nullptr, dwl ? dwl + off : nullptr}; }
   bool bf16_mode() const { return cfg.precision != MOCR_PRECISION_FP32; }
-  // decoder: head projections fused into the attention kernels (MOCR_DEC_FUSED=0: separate)
-  const bool fused_attn = getenv("MOCR_DEC_FUSED") == nullptr || atoi(getenv("MOCR_DEC_FUSED")) != 0;
+  // Greedy decoder: separate head-projection rowgemms + attention kernels by default.  The
+  // fused projection+attention kernel (one workgroup per (row, head)) re-reads the head's
+  // weight slice per row (48 MB of L2 traffic per self-attention layer at B = 64) and
+  // measured slower (decode-only, 3 replicas: 2757 vs 3230 img/s); MOCR_DEC_FUSED=1
+  // selects it.  Beam search always uses it (slot-table keys, shared image memory).
+  const bool fused_attn = getenv("MOCR_DEC_FUSED") != nullptr && atoi(getenv("MOCR_DEC_FUSED")) != 0;
   int attn_passes() const {
     return cfg.precision == MOCR_PRECISION_FP32 ? 0 : (cfg.precision == MOCR_PRECISION_BF16X3 ? 3 : 1);
   }
@@ -652,6 +656,7 @@ struct mocr_engine {
   // search: self-attention keys through `slots`, memory row = row / mem_div).
   void record_layers(int B, int t, const DecodeState* stp, const int32_t* slots, int mem_div) {
     const int d = cfg.d_model, L = cfg.n_layers;
+    const bool fused = fused_attn || slots != nullptr || mem_div != 1;
     const size_t cache_layer = (size_t)max_rows * cfg.max_pos * d;
     const size_t kv_layer = (size_t)cfg.max_batch * M * 2 * d;
     hipStream_t s = stream;
@@ -688,7 +693,7 @@ struct mocr_engine {
       const float* xin_s = l ? ds_ff : nullptr;
       // self-attention block: y_sa = x + SA(x)
       RowGemmParams p = base();
-      if (fused_attn) {
+      if (fused) {
         ProjAttnParams a = pa_base();
         a.A = xin; a.a_ln_g = xin_g; a.a_ln_b = xin_b; a.a_stats = xin_s; a.W = W(w.sa_inw); a.bias = W(w.sa_inb);
         a.K = kc; a.V = vc; a.kv_b_stride = (size_t)cfg.max_pos * d; a.kv_row_stride = d; a.n_cached = t;
@@ -708,7 +713,7 @@ struct mocr_engine {
       launch_rowgemm(p, s);
       // cross-attention block: y_ca = LN1(y_sa) + MHA(LN1(y_sa), mem)
       const float* memk = MEMKV + l * kv_layer;
-      if (fused_attn) {
+      if (fused) {
         ProjAttnParams a = pa_base();
         a.A = dy_sa; a.a_ln_g = W(w.n1w); a.a_ln_b = W(w.n1b); a.a_stats = ds_sa; a.W = W(w.ca_inw);
         a.bias = W(w.ca_inb); a.K = memk; a.V = memk + d; a.kv_b_stride = (size_t)M * 2 * d; a.kv_row_stride = 2 * d;

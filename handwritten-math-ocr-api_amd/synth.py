@@ -65,6 +65,34 @@ def _uniform(rng, shape, bound):
     return rng.uniform(-bound, bound, size=shape)
 
 
+def decoder_specs(vocab: int, max_pos: int, n_layers: int, d_model: int = D_MODEL, d_ff: int = D_FF,
+                  stack: str = "decoder.decoder.layers"):
+    """The decoder's tensors (shared by both encoder variants; only the layer-stack
+    name differs: ``decoder.decoder`` in src/model_swin.py:64, ``decoder.transformer_decoder``
+    in src/model_res18trans.py:79)."""
+    specs = []
+    add = specs.append
+    add(("decoder.embedding.weight", (vocab, d_model), "emb", 0))
+    add(("decoder.pos_encoder.weight", (max_pos, d_model), "emb", 0))
+    for l in range(n_layers):
+        p = f"{stack}.{l}."
+        for att in ("self_attn", "multihead_attn"):
+            add((p + att + ".in_proj_weight", (3 * d_model, d_model), "xavier", 0))
+            add((p + att + ".in_proj_bias", (3 * d_model,), "zero_b", 0))
+            add((p + att + ".out_proj.weight", (d_model, d_model), "lin_w", d_model))
+            add((p + att + ".out_proj.bias", (d_model,), "zero_b", 0))
+        add((p + "linear1.weight", (d_ff, d_model), "lin_w", d_model))
+        add((p + "linear1.bias", (d_ff,), "lin_b", d_model))
+        add((p + "linear2.weight", (d_model, d_ff), "lin_w", d_ff))
+        add((p + "linear2.bias", (d_model,), "lin_b", d_ff))
+        for n in (1, 2, 3):
+            add((p + f"norm{n}.weight", (d_model,), "ln_w", 0))
+            add((p + f"norm{n}.bias", (d_model,), "ln_b", 0))
+    add(("decoder.fc_out.weight", (vocab, d_model), "lin_w", d_model))
+    add(("decoder.fc_out.bias", (vocab,), "lin_b", d_model))
+    return specs
+
+
 def param_specs(vocab: int = VOCAB, max_pos: int = MAX_POS, n_layers: int = N_LAYERS,
                 d_model: int = D_MODEL, d_ff: int = D_FF):
     """Ordered (name, shape, init-kind, fan_in) for every tensor the hot path uses.
@@ -104,29 +132,12 @@ def param_specs(vocab: int = VOCAB, max_pos: int = MAX_POS, n_layers: int = N_LA
             dim *= 2
     add(("encoder.projection.weight", (d_model, ENC_DIM), "lin_w", ENC_DIM))
     add(("encoder.projection.bias", (d_model,), "lin_b", ENC_DIM))
-    add(("decoder.embedding.weight", (vocab, d_model), "emb", 0))
-    add(("decoder.pos_encoder.weight", (max_pos, d_model), "emb", 0))
-    for l in range(n_layers):
-        p = f"decoder.decoder.layers.{l}."
-        for att in ("self_attn", "multihead_attn"):
-            add((p + att + ".in_proj_weight", (3 * d_model, d_model), "xavier", 0))
-            add((p + att + ".in_proj_bias", (3 * d_model,), "zero_b", 0))
-            add((p + att + ".out_proj.weight", (d_model, d_model), "lin_w", d_model))
-            add((p + att + ".out_proj.bias", (d_model,), "zero_b", 0))
-        add((p + "linear1.weight", (d_ff, d_model), "lin_w", d_model))
-        add((p + "linear1.bias", (d_ff,), "lin_b", d_model))
-        add((p + "linear2.weight", (d_model, d_ff), "lin_w", d_ff))
-        add((p + "linear2.bias", (d_model,), "lin_b", d_ff))
-        for n in (1, 2, 3):
-            add((p + f"norm{n}.weight", (d_model,), "ln_w", 0))
-            add((p + f"norm{n}.bias", (d_model,), "ln_b", 0))
-    add(("decoder.fc_out.weight", (vocab, d_model), "lin_w", d_model))
-    add(("decoder.fc_out.bias", (vocab,), "lin_b", d_model))
+    specs += decoder_specs(vocab, max_pos, n_layers, d_model, d_ff)
     return specs
 
 
 def make_weights(seed: int = 1234, variant: str = "init", tied: bool = False,
-                 vocab: int = VOCAB, max_pos: int = MAX_POS, n_layers: int = N_LAYERS):
+                 vocab: int = VOCAB, max_pos: int = MAX_POS, n_layers: int = N_LAYERS, arch: str = "swin"):
     """Return an OrderedDict name -> float32 ndarray (blob order)."""
     if variant not in ("init", "perturbed"):
         raise ValueError(f"unknown variant {variant!r}")
@@ -134,7 +145,13 @@ def make_weights(seed: int = 1234, variant: str = "init", tied: bool = False,
     rng = np.random.Generator(np.random.PCG64(seed))
     out = OrderedDict()
     first_layer = {}
-    for name, shape, kind, fan_in in param_specs(vocab, max_pos, n_layers):
+    if arch == "swin":
+        specs = param_specs(vocab, max_pos, n_layers)
+    elif arch == "res18trans":
+        specs = param_specs_res18(vocab, max_pos)
+    else:
+        raise ValueError(f"unknown arch {arch!r}")
+    for name, shape, kind, fan_in in specs:
         if tied and name.startswith("decoder.decoder.layers.") and not name.startswith("decoder.decoder.layers.0."):
             suffix = name.split(".", 4)[4]
             out[name] = first_layer[suffix].copy()
@@ -164,6 +181,21 @@ def make_weights(seed: int = 1234, variant: str = "init", tied: bool = False,
             a = _uniform(rng, shape, 0.05) if pert else np.zeros(shape)
         elif kind == "emb":
             a = rng.standard_normal(shape)
+        elif kind == "res_conv":
+            # torchvision ResNet: kaiming_normal_(mode="fan_out", nonlinearity="relu")
+            a = rng.standard_normal(shape) * math.sqrt(2.0 / (shape[0] * shape[2] * shape[3]))
+        elif kind == "res_conv1":
+            # the 3-channel conv1 [64,3,7,7] averaged over RGB (src/model_res18trans.py:28-30)
+            w3 = rng.standard_normal((shape[0], 3) + shape[2:]) * math.sqrt(2.0 / (shape[0] * 49))
+            a = w3.mean(axis=1, keepdims=True)
+        elif kind == "bn_w":
+            a = np.ones(shape) + (0.1 * rng.standard_normal(shape) if pert else 0.0)
+        elif kind == "bn_b":
+            a = 0.05 * rng.standard_normal(shape) if pert else np.zeros(shape)
+        elif kind == "bn_mean":
+            a = 0.1 * rng.standard_normal(shape) if pert else np.zeros(shape)
+        elif kind == "bn_var":
+            a = rng.uniform(0.5, 1.5, size=shape) if pert else np.ones(shape)
         else:  # pragma: no cover
             raise AssertionError(kind)
         a = np.ascontiguousarray(a, dtype=np.float32)
@@ -220,3 +252,68 @@ def synthetic_vocab(vocab: int = VOCAB):
     toks = toks[:vocab]
     v = {t: k for k, t in enumerate(toks)}
     return v, {k: t for t, k in v.items()}
+
+
+# ResNet18 + Transformer-encoder variant (src/model_res18trans.py:13-64, BASELINE config 5).
+RES_CH = (64, 128, 256, 512)
+RES_ENC_LAYERS = 8   # src/config.py:28
+RES_DEC_LAYERS = 8   # src/config.py:29
+
+
+def param_specs_res18(vocab: int = VOCAB, max_pos: int = MAX_POS, n_enc: int = RES_ENC_LAYERS,
+                      n_dec: int = RES_DEC_LAYERS, d_model: int = D_MODEL, d_ff: int = D_FF):
+    """Blob order of the ResNet18-trans model: ``encoder.features`` = torchvision
+    resnet18 children [conv1, bn1, relu, maxpool, layer1..4] (indices 0..7), the
+    projection, the 8 post-norm ``TransformerEncoderLayer`` (batch_first), then the
+    decoder.  BatchNorm running statistics are part of the blob (eval BN)."""
+    specs = []
+    add = specs.append
+
+    def bn(p, c):
+        add((p + ".weight", (c,), "bn_w", 0))
+        add((p + ".bias", (c,), "bn_b", 0))
+        add((p + ".running_mean", (c,), "bn_mean", 0))
+        add((p + ".running_var", (c,), "bn_var", 0))
+
+    add(("encoder.features.0.weight", (64, 1, 7, 7), "res_conv1", 0))
+    bn("encoder.features.1", 64)
+    cin = 64
+    for li, c in enumerate(RES_CH):
+        for blk in range(2):
+            p = f"encoder.features.{4 + li}.{blk}."
+            stride = 2 if (li > 0 and blk == 0) else 1
+            add((p + "conv1.weight", (c, cin if blk == 0 else c, 3, 3), "res_conv", 0))
+            bn(p + "bn1", c)
+            add((p + "conv2.weight", (c, c, 3, 3), "res_conv", 0))
+            bn(p + "bn2", c)
+            if blk == 0 and (stride != 1 or cin != c):
+                add((p + "downsample.0.weight", (c, cin, 1, 1), "res_conv", 0))
+                bn(p + "downsample.1", c)
+        cin = c
+    add(("encoder.projection.weight", (d_model, 512), "lin_w", 512))
+    add(("encoder.projection.bias", (d_model,), "lin_b", 512))
+    for l in range(n_enc):
+        p = f"encoder.transformer_encoder.layers.{l}."
+        add((p + "self_attn.in_proj_weight", (3 * d_model, d_model), "xavier", 0))
+        add((p + "self_attn.in_proj_bias", (3 * d_model,), "zero_b", 0))
+        add((p + "self_attn.out_proj.weight", (d_model, d_model), "lin_w", d_model))
+        add((p + "self_attn.out_proj.bias", (d_model,), "zero_b", 0))
+        add((p + "linear1.weight", (d_ff, d_model), "lin_w", d_model))
+        add((p + "linear1.bias", (d_ff,), "lin_b", d_model))
+        add((p + "linear2.weight", (d_model, d_ff), "lin_w", d_ff))
+        add((p + "linear2.bias", (d_model,), "lin_b", d_ff))
+        for n in (1, 2):
+            add((p + f"norm{n}.weight", (d_model,), "ln_w", 0))
+            add((p + f"norm{n}.bias", (d_model,), "ln_b", 0))
+    specs += decoder_specs(vocab, max_pos, n_dec, d_model, d_ff, stack="decoder.transformer_decoder.layers")
+    return specs
+
+
+def make_pos_table(seed: int, tokens: int = 12, d_model: int = D_MODEL):
+    """The per-forward positional table of the ResNet18-trans encoder
+    (src/model_res18trans.py:57-59 draws ``nn.Embedding(tokens, d_model)``, i.e. N(0,1),
+    from torch's global RNG inside every forward).  The engine takes it as an input;
+    this is the table torch draws right after ``torch.manual_seed(seed)``."""
+    import torch
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(tokens, d_model, generator=g).numpy().astype(np.float32)

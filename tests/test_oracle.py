@@ -93,3 +93,35 @@ def test_shift_mask_regions(pH, pW, sh, sw):
     a = ref.reshape(-1)
     b = dev.reshape(-1)
     assert np.array_equal(a[:, None] == a[None, :], b[:, None] == b[None, :])
+
+
+@pytest.mark.parametrize("name", ["r384_b8_pert", "r96x320_b4_eos"])
+def test_res18_oracle_reproduces_golden(pkg, golden, name):
+    """ResNet18-trans (BASELINE config 5): the restatement reproduces the fixtures the
+    reference's own src/model_res18trans.py + src/inference.py produced."""
+    from oracle import res18_ref
+    g = golden(name)
+    m = g["meta"]
+    w = apply_eos_boost(pkg.synth.make_weights(m["seed"], m["variant"], arch="res18trans"), m["eos_boost"])
+    model = res18_ref.build_model(w)
+    imgs = torch.from_numpy(pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m["img_kind"]))
+    pos = torch.from_numpy(pkg.synth.make_pos_table(m["pos_seed"], g["memory"].shape[1]))
+    with torch.no_grad():
+        mem = model.encoder(imgs, pos)
+    np.testing.assert_allclose(mem.numpy(), g["memory"], rtol=0, atol=1e-5)
+    ys, logits = model_ref.greedy_decode(model, memory=mem, max_steps=m["steps"], stop=m["stop"], record_logits=True)
+    np.testing.assert_array_equal(ys.numpy(), g["ids"])
+    np.testing.assert_allclose(torch.stack(logits, 1)[:, :g["logits"].shape[1]].numpy(), g["logits"], atol=1e-5)
+
+
+def test_res18_encoder_attends_across_the_batch(pkg):
+    """Quirk of src/model_res18trans.py:61-62 (batch_first=True on a [w, B, d] tensor):
+    an image's memory depends on the other images of its batch."""
+    from oracle import res18_ref
+    model = res18_ref.build_model(pkg.synth.make_weights(3, "perturbed", arch="res18trans"))
+    imgs = torch.from_numpy(pkg.synth.make_images(3, 96, 320, seed0=1000))
+    pos = torch.from_numpy(pkg.synth.make_pos_table(1, 10))
+    with torch.no_grad():
+        full = model.encoder(imgs, pos)
+        alone = model.encoder(imgs[:1], pos)
+    assert not torch.allclose(full[:1], alone, atol=1e-3)
