@@ -249,11 +249,14 @@ __global__ void __launch_bounds__(256) dec_embed0_kernel(const int32_t* __restri
 // rescaling by exp(m_w - m); the result is Σ e v / Σ e, normalised at the end as in
 // the CPU flash-attention SDPA kernel the reference's F.multi_head_attention_forward
 // reaches.
+// q row b at q + b*q_ld; K/V rows of row b start at row (kv_mod ? b % kv_mod : b) times
+// kv_b_stride (kv_mod: the ResNet18-trans encoder, whose attention runs across the
+// images of a position: rows b*M + w attend to rows b'*M + w).
 template <int HB, int NIT>
 __global__ void __launch_bounds__(256) dec_attn_kernel(const DecodeState* st, int t, const float* __restrict__ q,
                                                        const float* __restrict__ K, const float* __restrict__ V,
                                                        size_t kv_b_stride, int kv_row_stride, int n,
-                                                       float* __restrict__ out, int d) {
+                                                       float* __restrict__ out, int d, int q_ld, int kv_mod) {
   constexpr int DIMS = 32 * HB;
   constexpr int LPR = DIMS / 4;  // lanes per key row
   constexpr int RPW = 64 / LPR;  // key rows per wave instruction
@@ -270,9 +273,10 @@ __global__ void __launch_bounds__(256) dec_attn_kernel(const DecodeState* st, in
   const int c4 = li * 4;
   const int hl = c4 / 32;
 
-  const floatx4 q4 = *reinterpret_cast<const floatx4*>(q + (size_t)b * d + hg * DIMS + c4);
-  const float* Kb = K + (size_t)b * kv_b_stride + hg * DIMS + c4;
-  const float* Vb = V + (size_t)b * kv_b_stride + hg * DIMS + c4;
+  const floatx4 q4 = *reinterpret_cast<const floatx4*>(q + (size_t)b * q_ld + hg * DIMS + c4);
+  const size_t kvb = (size_t)(kv_mod ? b % kv_mod : b);
+  const float* Kb = K + kvb * kv_b_stride + hg * DIMS + c4;
+  const float* Vb = V + kvb * kv_b_stride + hg * DIMS + c4;
   const int m_first = wave * RPW + rsub;
 
   floatx4 kk[NIT], vv[NIT];
@@ -722,6 +726,19 @@ __global__ void __launch_bounds__(256) beam_select_kernel(BeamParams p) {
   }
 }
 
+// ------------------------------------------------------------------ LayerNorm rows
+// out[r] = LN(y[r]) from the producer's slice statistics (row_stats_16lanes, the same
+// values every fused consumer computes): the ResNet18-trans encoder memory.
+__global__ void __launch_bounds__(256) ln_rows_kernel(const float* __restrict__ y, const float* __restrict__ stats,
+                                                      const float* __restrict__ g, const float* __restrict__ b,
+                                                      float* __restrict__ out) {
+  const int r = blockIdx.x;
+  const int c = threadIdx.x;
+  float mean, rstd;
+  row_stats_16lanes(stats + (size_t)r * 2 * kSlices, c & 15, mean, rstd);
+  out[(size_t)r * kD + c] = ln_apply(y[(size_t)r * kD + c], mean, rstd, g[c], b[c]);
+}
+
 // ------------------------------------------------------------------ greedy select
 // argmax over the vocabulary (first maximal index, as torch.argmax), log-prob of the
 // chosen token log(softmax + 1e-10) (app/src/im2latex.py:33-39), EOS bookkeeping for
@@ -840,14 +857,15 @@ void launch_dec_embed0(const int32_t* feed, int ld_ids, const float* emb, const 
 
 void launch_dec_attn(const DecodeState* st, int t, const float* q, const float* K, const float* V,
                      size_t kv_b_stride, int kv_row_stride, int n_fixed, int n_max, float* out, int B, int d,
-                     int heads, hipStream_t s) {
+                     int heads, hipStream_t s, int q_ld, int kv_mod) {
   constexpr int HB = 1;
   if (d != kD || heads * 32 != d) throw std::runtime_error("dec_attn: d_model 256 with 8 heads of 32");
   if (n_max > 256 || n_fixed < 1) throw std::runtime_error("dec_attn: 1..256 keys");
   const int nit = (n_max + 31) / 32;  // 32 key rows per workgroup pass (4 waves x 8 rows)
   const dim3 grid(B, heads / HB);
 #define MOCR_ATTN(N) \
-  dec_attn_kernel<HB, N><<<grid, 256, 0, s>>>(st, t, q, K, V, kv_b_stride, kv_row_stride, n_fixed, out, d)
+  dec_attn_kernel<HB, N><<<grid, 256, 0, s>>>(st, t, q, K, V, kv_b_stride, kv_row_stride, n_fixed, out, d, \
+                                               q_ld ? q_ld : d, kv_mod)
   switch (nit) {
     case 1: MOCR_ATTN(1); break;
     case 2: MOCR_ATTN(2); break;
@@ -910,6 +928,13 @@ void launch_beam_select(const BeamParams& p, hipStream_t s) {
     case 8: beam_select_kernel<8><<<p.B, 256, 0, s>>>(p); break;
     default: throw std::runtime_error("beam: 1..8 hypotheses per image");
   }
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_ln_rows(const float* y, const float* stats, const float* g, const float* b, float* out, int rows,
+                    hipStream_t s) {
+  if (rows <= 0) return;
+  ln_rows_kernel<<<rows, kD, 0, s>>>(y, stats, g, b, out);
   MOCR_HIP_CHECK(hipGetLastError());
 }
 

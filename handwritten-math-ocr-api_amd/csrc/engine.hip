@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -44,11 +45,38 @@ struct DecLayerW {
       n3b;
 };
 
-// Blob layout: the order of synth.py:param_specs.
+// ResNet18-trans pieces (synth.py:param_specs_res18 order).
+struct ConvW {
+  size_t w, bn_w, bn_b, bn_m, bn_v;
+  int cin, cout, ks, stride;
+};
+struct ResBlockW {
+  ConvW c1, c2, ds;
+  bool has_ds;
+};
+struct EncLayerW {
+  size_t inw, inb, ow, ob, l1w, l1b, l2w, l2b, n1w, n1b, n2w, n2b;
+};
+constexpr int kResCh[4] = {64, 128, 256, 512};
+
+// ResNet18 map sizes: conv1 /2 then maxpool /2 (H/4 for H % 4 == 0), then 3 stride-2 stages.
+inline int res_out(int n, int k, int s, int p) { return (n + 2 * p - k) / s + 1; }
+inline int res_h1(int h) { return res_out(res_out(h, 7, 2, 3), 3, 2, 1); }
+inline int res_h4(int h) {
+  h = res_h1(h);
+  for (int i = 0; i < 3; ++i) h = res_out(h, 3, 2, 1);
+  return h;
+}
+
+// Blob layout: the order of synth.py:param_specs (Swin) / param_specs_res18.
 struct Layout {
+  int arch = MOCR_ARCH_SWIN;
   size_t stem_w, stem_b, stem_lnw, stem_lnb;
   std::vector<SwinBlockW> blocks;  // 12
   MergeW merge[3];
+  ConvW r_conv1{};
+  std::vector<ResBlockW> rblocks;  // 8
+  std::vector<EncLayerW> elayers;  // 8
   size_t projw, projb, emb, pos;
   std::vector<DecLayerW> layers;
   size_t fcw, fcb;
@@ -62,6 +90,58 @@ struct Layout {
       return o;
     };
     const size_t d = c.d_model, ff = c.d_ff, V = c.vocab;
+    arch = c.arch;
+    if (arch == MOCR_ARCH_RES18TRANS) {
+      auto conv = [&](int cin, int cout, int ks, int stride) {
+        ConvW w;
+        w.w = take((size_t)cout * cin * ks * ks);
+        w.bn_w = take(cout);
+        w.bn_b = take(cout);
+        w.bn_m = take(cout);
+        w.bn_v = take(cout);
+        w.cin = cin;
+        w.cout = cout;
+        w.ks = ks;
+        w.stride = stride;
+        return w;
+      };
+      r_conv1 = conv(1, 64, 7, 2);
+      int cin = 64;
+      for (int li = 0; li < 4; ++li) {
+        const int ch = kResCh[li];
+        for (int blk = 0; blk < 2; ++blk) {
+          const int stride = (li > 0 && blk == 0) ? 2 : 1;
+          ResBlockW b{};
+          b.c1 = conv(blk == 0 ? cin : ch, ch, 3, stride);
+          b.c2 = conv(ch, ch, 3, 1);
+          b.has_ds = blk == 0 && (stride != 1 || cin != ch);
+          if (b.has_ds) b.ds = conv(cin, ch, 1, stride);
+          rblocks.push_back(b);
+        }
+        cin = ch;
+      }
+      projw = take(d * 512);
+      projb = take(d);
+      for (int l = 0; l < 8; ++l) {
+        EncLayerW e;
+        e.inw = take(3 * d * d);
+        e.inb = take(3 * d);
+        e.ow = take(d * d);
+        e.ob = take(d);
+        e.l1w = take(ff * d);
+        e.l1b = take(ff);
+        e.l2w = take(d * ff);
+        e.l2b = take(d);
+        e.n1w = take(d);
+        e.n1b = take(d);
+        e.n2w = take(d);
+        e.n2b = take(d);
+        elayers.push_back(e);
+      }
+      decoder_part(c, take);
+      total = off;
+      return;
+    }
     stem_w = take(kEmbed * 16);
     stem_b = take(kEmbed);
     stem_lnw = take(kEmbed);
@@ -94,6 +174,13 @@ struct Layout {
     }
     projw = take(d * kEncDim);
     projb = take(d);
+    decoder_part(c, take);
+    total = off;
+  }
+
+  template <typename Take>
+  void decoder_part(const mocr_config& c, Take& take) {
+    const size_t d = c.d_model, ff = c.d_ff, V = c.vocab;
     emb = take(V * d);
     pos = take((size_t)c.max_pos * d);
     for (int l = 0; l < c.n_layers; ++l) {
@@ -120,7 +207,6 @@ struct Layout {
     }
     fcw = take(V * d);
     fcb = take(V);
-    total = off;
   }
 };
 
@@ -135,6 +221,11 @@ void check_config(const mocr_config& c) {
   req(c.n_layers >= 1 && c.n_layers <= 64, "n_layers");
   req(c.max_pos >= 2 && c.max_pos <= 288, "max_pos in [2,288]");
   req(c.max_beam >= 0 && c.max_beam <= 8, "max_beam in [0,8]");
+  req(c.arch == MOCR_ARCH_SWIN || c.arch == MOCR_ARCH_RES18TRANS, "arch");
+  if (c.arch == MOCR_ARCH_RES18TRANS) {
+    req(c.img_h >= 32 && c.img_w >= 32, "ResNet18 needs images of at least 32x32");
+    req(c.max_batch <= 256, "ResNet18-trans: the encoder attends across at most 256 images");
+  }
   req(c.max_batch >= 1 && c.max_batch <= 4096, "max_batch");
   req(c.precision == MOCR_PRECISION_FP32 || c.precision == MOCR_PRECISION_BF16 ||
           c.precision == MOCR_PRECISION_BF16X3,
@@ -236,6 +327,7 @@ struct mocr_engine {
   std::vector<hipEvent_t> event_pool;
 
   ~mocr_engine() {
+    free_res18();
     (void)hipSetDevice(device);
     for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
     for (auto e : event_pool) (void)hipEventDestroy(e);
@@ -260,6 +352,272 @@ struct mocr_engine {
 
   const float* W(size_t off) const { return dw + off; }
 
+  // ---------------------------------------------------------------- ResNet18-trans state
+  struct DevConv {
+    uint16_t* wh = nullptr;  // [cout][ks][ks][cin] BN-folded, bf16 hi / lo planes
+    uint16_t* wl = nullptr;
+    float* bias = nullptr;   // BN shift
+    int cin = 0, cout = 0, ks = 0, stride = 1;
+  };
+  struct DevBlock {
+    DevConv c1, c2, ds;
+    bool has_ds = false;
+  };
+  std::vector<DevBlock> rdev;
+  float* rstem_w = nullptr;  // [64][49] BN-folded conv1
+  float* rstem_b = nullptr;
+  float* RX[2] = {nullptr, nullptr};           // fp32 block input / identity maps (NHWC)
+  uint16_t *RXh = nullptr, *RXl = nullptr;     // planes of the block input
+  uint16_t *RTh = nullptr, *RTl = nullptr;     // planes of a block's conv1 output
+  void* rzero = nullptr;                       // zero taps of the implicit-GEMM convs
+  float *RP = nullptr, *RPOS = nullptr, *RPOSB = nullptr;  // pooled rows, pos table, replicated table
+  float *EX0 = nullptr, *EQKV = nullptr, *EATT = nullptr, *EY1 = nullptr, *EY2 = nullptr, *EH = nullptr;
+  float *ES0 = nullptr, *ES1 = nullptr, *ES2 = nullptr;  // LayerNorm slice stats [rows][16][2]
+  bool pos_set = false;
+  int rH1 = 0, rW1 = 0, rH4 = 0;
+
+  bool res_x3() const { return cfg.precision != MOCR_PRECISION_BF16; }  // conv passes: 3 unless plain bf16
+
+  void init_res18() {
+    const size_t B = cfg.max_batch, d = cfg.d_model, L = cfg.n_layers;
+    rH1 = res_h1(cfg.img_h);
+    rW1 = res_h1(cfg.img_w);
+    rH4 = res_h4(cfg.img_h);
+    M = res_h4(cfg.img_w);
+    Hm = 1;
+    Wm = M;
+    const size_t rows = B * M;
+    // the largest NHWC map is layer1's (channels double as the map quarters)
+    const size_t szmap = B * (size_t)rH1 * rW1 * 64;
+    dw = dalloc<float>(lay->total);
+    fcw_pad = dalloc<float>((size_t)Vpad * d);
+    fcb_pad = dalloc<float>(Vpad);
+    kvw_all = dalloc<float>(L * 2 * d * d);
+    kvb_all = dalloc<float>(L * 2 * d);
+    img = dalloc<float>(B * cfg.img_h * cfg.img_w);
+    MEM = dalloc<float>(rows * d);
+    MEMKV = dalloc<float>(rows * L * 2 * d);
+    RX[0] = dalloc<float>(szmap);
+    RX[1] = dalloc<float>(szmap);
+    RXh = dalloc<uint16_t>(szmap);
+    RTh = dalloc<uint16_t>(szmap);
+    if (res_x3()) {
+      RXl = dalloc<uint16_t>(szmap);
+      RTl = dalloc<uint16_t>(szmap);
+    }
+    rzero = dalloc<char>(256);
+    MOCR_HIP_CHECK(hipMemset(rzero, 0, 256));
+    RP = dalloc<float>(rows * 512);
+    RPOS = dalloc<float>((size_t)M * d);
+    RPOSB = dalloc<float>(rows * d);
+    EX0 = dalloc<float>(rows * d);
+    EQKV = dalloc<float>(rows * 3 * d);
+    EATT = dalloc<float>(rows * d);
+    EY1 = dalloc<float>(rows * d);
+    EY2 = dalloc<float>(rows * d);
+    EH = dalloc<float>(rows * cfg.d_ff);
+    ES0 = dalloc<float>(rows * 32);
+    ES1 = dalloc<float>(rows * 32);
+    ES2 = dalloc<float>(rows * 32);
+    rstem_w = dalloc<float>(64 * 49);
+    rstem_b = dalloc<float>(64);
+    for (const ResBlockW& b : lay->rblocks) {
+      DevBlock db;
+      auto mk = [&](const ConvW& c) {
+        DevConv dc;
+        const size_t n = (size_t)c.cout * c.ks * c.ks * c.cin;
+        dc.wh = dalloc<uint16_t>(n);
+        if (res_x3()) dc.wl = dalloc<uint16_t>(n);
+        dc.bias = dalloc<float>(c.cout);
+        dc.cin = c.cin;
+        dc.cout = c.cout;
+        dc.ks = c.ks;
+        dc.stride = c.stride;
+        return dc;
+      };
+      db.c1 = mk(b.c1);
+      db.c2 = mk(b.c2);
+      db.has_ds = b.has_ds;
+      if (b.has_ds) db.ds = mk(b.ds);
+      rdev.push_back(db);
+    }
+  }
+
+  void free_res18() {
+    for (DevBlock& b : rdev)
+      for (DevConv* c : {&b.c1, &b.c2, &b.ds})
+        for (void* q : {(void*)c->wh, (void*)c->wl, (void*)c->bias})
+          if (q) (void)hipFree(q);
+    void* bufs[] = {RX[0], RX[1], RXh, RXl, RTh, RTl, rzero, RP, RPOS, RPOSB, EX0, EQKV, EATT, EY1, EY2, EH, ES0, ES1,
+                    ES2, rstem_w, rstem_b};
+    for (void* q : bufs)
+      if (q) (void)hipFree(q);
+  }
+
+  // Eval BatchNorm folded into the conv (torch: y = (conv(x) - mean) / sqrt(var + eps) * g + b):
+  // w' = w * g / sqrt(var + eps) reordered to [cout][ky][kx][cin], bias = b - mean * g / sqrt(var + eps).
+  static void fold_bn(const float* blob, const ConvW& c, std::vector<float>& w, std::vector<float>& bias) {
+    const int K = c.ks * c.ks;
+    w.assign((size_t)c.cout * K * c.cin, 0.f);
+    bias.assign(c.cout, 0.f);
+    for (int o = 0; o < c.cout; ++o) {
+      const float sc = blob[c.bn_w + o] / std::sqrt(blob[c.bn_v + o] + 1e-5f);
+      bias[o] = blob[c.bn_b + o] - blob[c.bn_m + o] * sc;
+      for (int i = 0; i < c.cin; ++i)
+        for (int k = 0; k < K; ++k) w[((size_t)o * K + k) * c.cin + i] = blob[c.w + ((size_t)o * c.cin + i) * K + k] * sc;
+    }
+  }
+
+  void load_res18(const float* blob) {
+    std::vector<float> w, bias;
+    fold_bn(blob, lay->r_conv1, w, bias);
+    MOCR_HIP_CHECK(hipMemcpy(rstem_w, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+    MOCR_HIP_CHECK(hipMemcpy(rstem_b, bias.data(), bias.size() * 4, hipMemcpyHostToDevice));
+    float* tmp = dalloc<float>((size_t)512 * 512 * 9);
+    for (size_t i = 0; i < rdev.size(); ++i) {
+      const ResBlockW& b = lay->rblocks[i];
+      auto up = [&](const ConvW& c, DevConv& dc) {
+        fold_bn(blob, c, w, bias);
+        MOCR_HIP_CHECK(hipMemcpy(tmp, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+        launch_split_bf16(tmp, dc.wh, dc.wl, w.size(), stream);
+        MOCR_HIP_CHECK(hipStreamSynchronize(stream));
+        MOCR_HIP_CHECK(hipMemcpy(dc.bias, bias.data(), bias.size() * 4, hipMemcpyHostToDevice));
+      };
+      up(b.c1, rdev[i].c1);
+      up(b.c2, rdev[i].c2);
+      if (b.has_ds) up(b.ds, rdev[i].ds);
+    }
+    (void)hipFree(tmp);
+  }
+
+  void set_encoder_pos(const float* table, int tokens) {
+    if (cfg.arch != MOCR_ARCH_RES18TRANS) throw std::runtime_error("mocr_set_encoder_pos: only for MOCR_ARCH_RES18TRANS");
+    if (tokens != M) throw std::runtime_error("positional table has " + std::to_string(tokens) + " rows, the encoder "
+                                              "makes " + std::to_string(M) + " tokens");
+    MOCR_HIP_CHECK(hipSetDevice(device));
+    MOCR_HIP_CHECK(hipMemcpy(RPOS, table, (size_t)M * cfg.d_model * 4, hipMemcpyHostToDevice));
+    pos_set = true;
+    encoded = false;
+  }
+
+  // One implicit-GEMM conv: NHWC [B, h, w, cin] planes -> [B, ho, wo, cout].
+  void conv(const char* name, const DevConv& c, const uint16_t* Ah, const uint16_t* Al, int B, int h, int w,
+            float* C, uint16_t* Ch, uint16_t* Cl, int epi) {
+    const int pad = c.ks / 2;
+    const int ho = res_out(h, c.ks, c.stride, pad), wo = res_out(w, c.ks, c.stride, pad);
+    GemmParams p{};
+    p.A = Ah;
+    p.A_lo = res_x3() ? Al : nullptr;
+    p.W = c.wh;
+    p.W_lo = res_x3() ? c.wl : nullptr;
+    p.bias = c.bias;
+    p.C = C;
+    p.C16 = Ch;
+    p.C16lo = res_x3() ? Cl : nullptr;
+    p.M = B * ho * wo;
+    p.N = c.cout;
+    p.K = c.ks * c.ks * c.cin;
+    p.lda = p.K;
+    p.ldw = p.K;
+    p.ldc = c.cout;
+    p.epi = epi;
+    p.conv = ConvGeom{1, h, w, c.cin, ho, wo, c.ks, c.stride, pad};
+    p.zero = rzero;
+    const double flops = 2.0 * p.M * p.N * p.K;
+    const double bytes = (res_x3() ? 4.0 : 2.0) * ((double)B * h * w * c.cin + (double)p.N * p.K) +
+                         4.0 * (double)p.M * p.N * (epi == EPI_RESRELU ? 3 : 1);
+    timed(name, flops, bytes, [&] { launch_gemm_bf16(p, stream); });
+  }
+
+  void encode_res18(int B) {
+    if (!pos_set) throw std::runtime_error("MOCR_ARCH_RES18TRANS: mocr_set_encoder_pos before mocr_encode");
+    const int d = cfg.d_model, rows = B * M;
+    static const char* c1n[] = {"l1.conv1", "l1.conv1", "l2.conv1", "l2.conv1", "l3.conv1", "l3.conv1", "l4.conv1",
+                                "l4.conv1"};
+    static const char* c2n[] = {"l1.conv2", "l1.conv2", "l2.conv2", "l2.conv2", "l3.conv2", "l3.conv2", "l4.conv2",
+                                "l4.conv2"};
+    static const char* dsn[] = {"", "", "l2.down", "", "l3.down", "", "l4.down", ""};
+    timed("r.stem", 2.0 * B * (res_out(cfg.img_h, 7, 2, 3) * (double)res_out(cfg.img_w, 7, 2, 3)) * 64 * 49,
+          4.0 * B * ((double)cfg.img_h * cfg.img_w + (double)rH1 * rW1 * 64 * (res_x3() ? 2 : 1.5)),
+          [&] { launch_res_stem(img, rstem_w, rstem_b, RX[0], RXh, RXl, B, cfg.img_h, cfg.img_w, stream); });
+    int h = rH1, w = rW1;
+    float* x = RX[0];
+    float* spare = RX[1];
+    for (size_t i = 0; i < rdev.size(); ++i) {
+      const DevBlock& b = rdev[i];
+      conv(c1n[i], b.c1, RXh, RXl, B, h, w, nullptr, RTh, RTl, EPI_RELU);
+      const int ho = res_out(h, 3, b.c1.stride, 1), wo = res_out(w, 3, b.c1.stride, 1);
+      float* ident = x;
+      if (b.has_ds) {
+        conv(dsn[i], b.ds, RXh, RXl, B, h, w, spare, nullptr, nullptr, EPI_STORE);
+        ident = spare;
+      }
+      conv(c2n[i], b.c2, RTh, RTl, B, ho, wo, ident, RXh, RXl, EPI_RESRELU);
+      if (b.has_ds) std::swap(x, spare);
+      h = ho;
+      w = wo;
+    }
+    // AdaptiveAvgPool2d((1, None)) -> [B*M, 512]; projection + positional table
+    timed("r.avgpool", 0, 4.0 * B * (double)h * w * 512, [&] { launch_res_avgpool(x, RP, B, h, w, 512, stream); });
+    launch_res_posrep(RPOS, RPOSB, rows, M, d, stream);
+    auto rg = [&]() {
+      RowGemmParams p{};
+      p.B = rows;
+      p.d = d;
+      p.max_pos = cfg.max_pos;
+      return p;
+    };
+    RowGemmParams p = rg();
+    p.A = RP; p.W = W(lay->projw); p.bias = W(lay->projb); p.resid = RPOSB; p.out = EX0; p.out_stats = ES0;
+    p.N = d; p.K = 512; p.ldo = d; p.n_valid = d; p.epi = DEC_RESADD;
+    timed("r.proj", 2.0 * rows * d * 512, 4.0 * (rows * 512.0 + d * 512.0 + 2.0 * rows * d),
+          [&] { launch_rowgemm(p, stream); });
+    // 8 post-norm TransformerEncoderLayers (batch_first on [M, B, d]: attention across images)
+    const float *xin = EX0, *xs = nullptr, *xg = nullptr, *xb = nullptr;
+    for (size_t l = 0; l < lay->elayers.size(); ++l) {
+      const EncLayerW& e = lay->elayers[l];
+      timed("r.enc", 2.0 * rows * 256.0 * (768 + 256 + 1024) + 4.0 * rows * (double)B * d,
+            4.0 * (rows * 256.0 * 12 + 256.0 * 256 * 8), [&] {
+        RowGemmParams q = rg();
+        q.A = xin; q.a_stats = xs; q.a_ln_g = xg; q.a_ln_b = xb; q.W = W(e.inw); q.bias = W(e.inb); q.out = EQKV;
+        q.N = 3 * d; q.K = d; q.ldo = 3 * d; q.n_valid = 3 * d; q.epi = DEC_STORE;
+        launch_rowgemm(q, stream);
+        launch_dec_attn(nullptr, 0, EQKV, EQKV + d, EQKV + 2 * d, (size_t)3 * d, M * 3 * d, B, B, EATT, rows, d,
+                        cfg.n_heads, stream, 3 * d, M);
+        q = rg();
+        q.A = EATT; q.W = W(e.ow); q.bias = W(e.ob); q.resid = xin; q.r_stats = xs; q.r_ln_g = xg; q.r_ln_b = xb;
+        q.out = EY1; q.out_stats = ES1; q.N = d; q.K = d; q.ldo = d; q.n_valid = d; q.epi = DEC_RESADD;
+        launch_rowgemm(q, stream);
+        q = rg();
+        q.A = EY1; q.a_stats = ES1; q.a_ln_g = W(e.n1w); q.a_ln_b = W(e.n1b); q.W = W(e.l1w); q.bias = W(e.l1b);
+        q.out = EH; q.N = cfg.d_ff; q.K = d; q.ldo = cfg.d_ff; q.n_valid = cfg.d_ff; q.epi = DEC_RELU;
+        launch_rowgemm(q, stream);
+        q = rg();
+        q.A = EH; q.W = W(e.l2w); q.bias = W(e.l2b); q.resid = EY1; q.r_stats = ES1; q.r_ln_g = W(e.n1w);
+        q.r_ln_b = W(e.n1b); q.out = EY2; q.out_stats = ES2; q.N = d; q.K = cfg.d_ff; q.ldo = d; q.n_valid = d;
+        q.epi = DEC_RESADD;
+        launch_rowgemm(q, stream);
+      });
+      xin = EY2;
+      xs = ES2;
+      xg = W(e.n2w);
+      xb = W(e.n2b);
+    }
+    // memory = LN2 of the last layer (materialised for mocr_get_memory) and every decoder
+    // layer's cross-attention K/V from it (LayerNorm applied on load)
+    launch_ln_rows(xin, xs, xg, xb, MEM, rows, stream);
+    const size_t kv_layer = (size_t)cfg.max_batch * M * 2 * d;
+    for (int l = 0; l < cfg.n_layers; ++l) {
+      const DecLayerW& dl = lay->layers[l];
+      RowGemmParams q = rg();
+      q.A = xin; q.a_stats = xs; q.a_ln_g = xg; q.a_ln_b = xb; q.W = W(dl.ca_inw) + (size_t)d * d;
+      q.bias = W(dl.ca_inb) + d; q.out = MEMKV + l * kv_layer; q.N = 2 * d; q.K = d; q.ldo = 2 * d;
+      q.n_valid = 2 * d; q.epi = DEC_STORE;
+      timed("crosskv", 2.0 * rows * 512 * 256, 4.0 * (rows * 256.0 + 512 * 256 + rows * 512.0),
+            [&] { launch_rowgemm(q, stream); });
+    }
+  }
+
   // ---------------------------------------------------------------- setup
   void init(const mocr_config& c, int dev) {
     check_config(c);
@@ -269,70 +627,75 @@ struct mocr_engine {
     MOCR_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     lay.reset(new Layout(cfg));
 
-    H1 = cfg.img_h / 4;
-    W1 = cfg.img_w / 4;
-    int H = H1, Wd = W1, C = kEmbed;
     const size_t B = cfg.max_batch;
-    for (int s = 0; s < kStages; ++s) {
-      stage[s] = make_win(H, Wd, C, kHeads[s]);
-      const WinGeom& wg = stage[s].win[0];
-      szX = std::max(szX, B * H * Wd * C);
-      szXW = std::max(szXW, B * wg.nWin * kWinTok * C);
-      szQKV = std::max(szQKV, B * wg.nWin * kWinTok * 3 * C);
-      szHID = std::max(szHID, B * H * Wd * 4 * C);
-      if (s < kStages - 1) {
-        const int Ho = (H + 1) / 2, Wo = (Wd + 1) / 2;
-        szXW = std::max(szXW, B * Ho * Wo * 4 * C);
-        szX = std::max(szX, B * Ho * Wo * 2 * C);
-        H = Ho;
-        Wd = Wo;
-        C *= 2;
-      }
-    }
-    Hm = H;
-    Wm = Wd;
-    M = Hm * Wm;
     Vpad = (cfg.vocab + 15) / 16 * 16;
     const size_t d = cfg.d_model, L = cfg.n_layers;
-
-    dw = dalloc<float>(lay->total);
-    relbias.assign(lay->blocks.size(), nullptr);
-    for (size_t i = 0, bi = 0; i < (size_t)kStages; ++i)
-      for (int j = 0; j < kDepth[i]; ++j, ++bi) relbias[bi] = dalloc<float>((size_t)kHeads[i] * kWinTok * kWinTok);
-    relmask.assign(lay->blocks.size(), nullptr);
-    if (cfg.precision != MOCR_PRECISION_FP32)
-      for (size_t i = 0, bi = 0; i < (size_t)kStages; ++i)
-        for (int j = 0; j < kDepth[i]; ++j, ++bi) relmask[bi] = dalloc<float>((size_t)4 * kHeads[i] * 64 * 64);
-    fcw_pad = dalloc<float>((size_t)Vpad * d);
-    fcb_pad = dalloc<float>(Vpad);
-    kvw_all = dalloc<float>(L * 2 * d * d);
-    kvb_all = dalloc<float>(L * 2 * d);
-
-    img = dalloc<float>(B * cfg.img_h * cfg.img_w);
-    X = dalloc<float>(szX);
-    X2 = dalloc<float>(szX);
-    XW = dalloc<float>(szXW);
-    ATT = dalloc<float>(szXW);
-    QKV = dalloc<float>(szQKV);
-    HID = dalloc<float>(szHID);
-    MEM = dalloc<float>(B * M * d);
-    MEMKV = dalloc<float>(B * M * L * 2 * d);
-    if (cfg.precision != MOCR_PRECISION_FP32) {
-      const bool x3 = cfg.precision == MOCR_PRECISION_BF16X3;
-      XWh = dalloc<uint16_t>(szXW);
-      ATTh = dalloc<uint16_t>(szXW);
-      HIDh = dalloc<uint16_t>(szHID);
-      MEMh = dalloc<uint16_t>(B * M * d);
-      dwh = dalloc<uint16_t>(lay->total);
-      kvwh = dalloc<uint16_t>(L * 2 * d * d);
-      if (x3) {
-        XWl = dalloc<uint16_t>(szXW);
-        ATTl = dalloc<uint16_t>(szXW);
-        HIDl = dalloc<uint16_t>(szHID);
-        MEMl = dalloc<uint16_t>(B * M * d);
-        dwl = dalloc<uint16_t>(lay->total);
-        kvwl = dalloc<uint16_t>(L * 2 * d * d);
+    if (cfg.arch == MOCR_ARCH_RES18TRANS) {
+      init_res18();
+    } else {
+      H1 = cfg.img_h / 4;
+      W1 = cfg.img_w / 4;
+      int H = H1, Wd = W1, C = kEmbed;
+      for (int s = 0; s < kStages; ++s) {
+        stage[s] = make_win(H, Wd, C, kHeads[s]);
+        const WinGeom& wg = stage[s].win[0];
+        szX = std::max(szX, B * H * Wd * C);
+        szXW = std::max(szXW, B * wg.nWin * kWinTok * C);
+        szQKV = std::max(szQKV, B * wg.nWin * kWinTok * 3 * C);
+        szHID = std::max(szHID, B * H * Wd * 4 * C);
+        if (s < kStages - 1) {
+          const int Ho = (H + 1) / 2, Wo = (Wd + 1) / 2;
+          szXW = std::max(szXW, B * Ho * Wo * 4 * C);
+          szX = std::max(szX, B * Ho * Wo * 2 * C);
+          H = Ho;
+          Wd = Wo;
+          C *= 2;
+        }
       }
+      Hm = H;
+      Wm = Wd;
+      M = Hm * Wm;
+
+      dw = dalloc<float>(lay->total);
+      relbias.assign(lay->blocks.size(), nullptr);
+      for (size_t i = 0, bi = 0; i < (size_t)kStages; ++i)
+        for (int j = 0; j < kDepth[i]; ++j, ++bi) relbias[bi] = dalloc<float>((size_t)kHeads[i] * kWinTok * kWinTok);
+      relmask.assign(lay->blocks.size(), nullptr);
+      if (cfg.precision != MOCR_PRECISION_FP32)
+        for (size_t i = 0, bi = 0; i < (size_t)kStages; ++i)
+          for (int j = 0; j < kDepth[i]; ++j, ++bi) relmask[bi] = dalloc<float>((size_t)4 * kHeads[i] * 64 * 64);
+      fcw_pad = dalloc<float>((size_t)Vpad * d);
+      fcb_pad = dalloc<float>(Vpad);
+      kvw_all = dalloc<float>(L * 2 * d * d);
+      kvb_all = dalloc<float>(L * 2 * d);
+
+      img = dalloc<float>(B * cfg.img_h * cfg.img_w);
+      X = dalloc<float>(szX);
+      X2 = dalloc<float>(szX);
+      XW = dalloc<float>(szXW);
+      ATT = dalloc<float>(szXW);
+      QKV = dalloc<float>(szQKV);
+      HID = dalloc<float>(szHID);
+      MEM = dalloc<float>(B * M * d);
+      MEMKV = dalloc<float>(B * M * L * 2 * d);
+      if (cfg.precision != MOCR_PRECISION_FP32) {
+        const bool x3 = cfg.precision == MOCR_PRECISION_BF16X3;
+        XWh = dalloc<uint16_t>(szXW);
+        ATTh = dalloc<uint16_t>(szXW);
+        HIDh = dalloc<uint16_t>(szHID);
+        MEMh = dalloc<uint16_t>(B * M * d);
+        dwh = dalloc<uint16_t>(lay->total);
+        kvwh = dalloc<uint16_t>(L * 2 * d * d);
+        if (x3) {
+          XWl = dalloc<uint16_t>(szXW);
+          ATTl = dalloc<uint16_t>(szXW);
+          HIDl = dalloc<uint16_t>(szHID);
+          MEMl = dalloc<uint16_t>(B * M * d);
+          dwl = dalloc<uint16_t>(lay->total);
+          kvwl = dalloc<uint16_t>(L * 2 * d * d);
+        }
+      }
+
     }
 
     // decoder rows: one per image (greedy) or per hypothesis (beam search)
@@ -404,10 +767,11 @@ struct mocr_engine {
                                std::to_string(lay->total));
     MOCR_HIP_CHECK(hipSetDevice(device));
     MOCR_HIP_CHECK(hipMemcpy(dw, blob, n * sizeof(float), hipMemcpyHostToDevice));
+    if (cfg.arch == MOCR_ARCH_RES18TRANS) load_res18(blob);
     // Expanded relative-position bias [h, 49, 49] = table[index(i, j), h]
     // (torchvision _get_relative_position_bias with relative_position_index).
     size_t bi = 0;
-    for (int s = 0; s < kStages; ++s) {
+    for (int s = 0; s < kStages && cfg.arch == MOCR_ARCH_SWIN; ++s) {
       const int h = kHeads[s];
       for (int j = 0; j < kDepth[s]; ++j, ++bi) {
         const float* table = blob + lay->blocks[bi].table;
@@ -561,6 +925,14 @@ struct mocr_engine {
     if (!weights_loaded) throw std::runtime_error("weights not loaded");
     if (B != cur_batch) throw std::runtime_error("batch differs from the uploaded images");
     MOCR_HIP_CHECK(hipSetDevice(device));
+    if (cfg.arch == MOCR_ARCH_RES18TRANS) {
+      if (stop_after >= 0) throw std::runtime_error("encode_until: Swin only");
+      encode_res18(B);
+      MOCR_HIP_CHECK(hipStreamSynchronize(stream));
+      if (timing) flush_timing();
+      encoded = true;
+      return;
+    }
     const size_t d = cfg.d_model, L = cfg.n_layers;
     timed("stem", 2.0 * B * H1 * W1 * kEmbed * 16, 4.0 * B * (cfg.img_h * cfg.img_w + (double)H1 * W1 * kEmbed),
           [&] { launch_stem(img, W(lay->stem_w), W(lay->stem_b), W(lay->stem_lnw), W(lay->stem_lnb), X, B,
@@ -988,6 +1360,7 @@ size_t mocr_weight_count(const mocr_config* cfg) {
 }
 
 int mocr_memory_tokens(const mocr_config* cfg) {
+  if (cfg->arch == MOCR_ARCH_RES18TRANS) return res_h4(cfg->img_w);  // one token per layer4 column
   int H = cfg->img_h / 4, W = cfg->img_w / 4;
   for (int s = 0; s < kStages - 1; ++s) {
     H = (H + 1) / 2;
@@ -1038,6 +1411,10 @@ int mocr_get_memory(mocr_engine* eng, float* host_out) {
     MOCR_HIP_CHECK(hipMemcpy(host_out, eng->MEM, (size_t)eng->cur_batch * eng->M * eng->cfg.d_model * sizeof(float),
                              hipMemcpyDeviceToHost));
   })
+}
+
+int mocr_set_encoder_pos(mocr_engine* eng, const float* table, int tokens) {
+  MOCR_API_BODY(eng, eng->set_encoder_pos(table, tokens))
 }
 
 int mocr_decode_beam(mocr_engine* eng, int beam, int max_steps, int stop_mode, int32_t* ids_out, float* scores_out,

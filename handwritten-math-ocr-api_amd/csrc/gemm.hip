@@ -290,7 +290,29 @@ __device__ __forceinline__ void epi_vec8(const GemmParams& p, int row, int col, 
       v[4 + e] += b1[e];
     }
   }
-  if constexpr (EPI == EPI_RESADD || EPI == EPI_WINRES) {
+  if constexpr (EPI == EPI_RESRELU) {
+    const size_t off = (size_t)row * p.ldc + col;
+    float* c = p.C + off;
+    const floatx4 r0 = *reinterpret_cast<const floatx4*>(c);
+    const floatx4 r1 = *reinterpret_cast<const floatx4*>(c + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = fmaxf(r0[e] + v[e], 0.f);
+      v[4 + e] = fmaxf(r1[e] + v[4 + e], 0.f);
+    }
+    *reinterpret_cast<floatx4*>(c) = floatx4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<floatx4*>(c + 4) = floatx4{v[4], v[5], v[6], v[7]};
+    if (p.C16) {
+      u16x8 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        hi[e] = bf16_rne(v[e]);
+        lo[e] = bf16_rne(v[e] - bf16_to_f32(hi[e]));
+      }
+      *reinterpret_cast<u16x8*>(static_cast<uint16_t*>(p.C16) + off) = hi;
+      if (p.C16lo) *reinterpret_cast<u16x8*>(static_cast<uint16_t*>(p.C16lo) + off) = lo;
+    }
+  } else if constexpr (EPI == EPI_RESADD || EPI == EPI_WINRES) {
     float* c;
     if constexpr (EPI == EPI_RESADD) {
       c = p.C + (size_t)row * p.ldc + col;
@@ -323,6 +345,10 @@ __device__ __forceinline__ void epi_vec8(const GemmParams& p, int row, int col, 
     if constexpr (EPI == EPI_GELU) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+    }
+    if constexpr (EPI == EPI_RELU) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
     }
     const size_t off = (size_t)row * p.ldc + col;
     if (p.C) {
@@ -487,7 +513,7 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 __device__ __forceinline__ int swz(int r) { return (0x1320 >> (4 * ((r >> 2) & 3))) & 3; }  // {0,2,3,1}
 
-template <int TM, int TN, int WGM, int WGN, int EPI, int PASSES, int NSTAGE>
+template <int TM, int TN, int WGM, int WGN, int EPI, int PASSES, int NSTAGE, bool CONV = false>
 __global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_ring_kernel(GemmParams p) {
   constexpr int BM = 16 * TM * WGM;
   constexpr int BN = 16 * TN * WGN;
@@ -527,17 +553,51 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_ring_kernel(GemmPara
   // per-lane DMA source: piece row = 16*piece + lane/4, chunk lane%4 (swizzled)
   const int prow = lane >> 2;
   const int pch = lane & 3;
+  // implicit-GEMM conv: this lane's output pixel per A piece -> input origin (iy0, ix0)
+  int cv_b[A_DMA], cv_iy[A_DMA], cv_ix[A_DMA];
+  if constexpr (CONV) {
+    const ConvGeom& g = p.conv;
+#pragma unroll
+    for (int i = 0; i < A_DMA; ++i) {
+      const int pc = min(wave * A_DMA + i, BM / 16 - 1);
+      const int gr = row0 + pc * 16 + prow;
+      const int hw = g.Hout * g.Wout;
+      const int b = gr / hw;
+      const int rem = gr - b * hw;
+      const int oy = rem / g.Wout;
+      cv_b[i] = gr < p.M ? b : -1;
+      cv_iy[i] = oy * g.stride - g.pad;
+      cv_ix[i] = (rem - oy * g.Wout) * g.stride - g.pad;
+    }
+  }
   auto issue = [&](int kt) {
     char* st = lds + (kt % NSTAGE) * STAGE;
     const int kb = kt * ROWB;
+    int ky = 0, kx = 0, c0 = 0;
+    if constexpr (CONV) {
+      const int k0 = kt * BK16;
+      const int tap = k0 / p.conv.Cin;
+      c0 = k0 - tap * p.conv.Cin;
+      ky = tap / p.conv.ks;
+      kx = tap - ky * p.conv.ks;
+    }
 #pragma unroll
     for (int q = 0; q < PL; ++q) {
 #pragma unroll
       for (int i = 0; i < A_DMA; ++i) {
         const int pc = min(wave * A_DMA + i, BM / 16 - 1);
         const int r = pc * 16 + prow;
-        const int gr = min(row0 + r, p.M - 1);
-        const char* src = Ag[q] + (size_t)gr * p.lda * 2 + kb + 16 * (pch ^ swz(r));
+        const char* src;
+        if constexpr (CONV) {
+          const ConvGeom& g = p.conv;
+          const int iy = cv_iy[i] + ky, ix = cv_ix[i] + kx;
+          const bool ok = cv_b[i] >= 0 && iy >= 0 && iy < g.Hin && ix >= 0 && ix < g.Win;
+          src = ok ? Ag[q] + ((((size_t)cv_b[i] * g.Hin + iy) * g.Win + ix) * g.Cin + c0) * 2 + 16 * (pch ^ swz(r))
+                   : static_cast<const char*>(p.zero) + 16 * pch;
+        } else {
+          const int gr = min(row0 + r, p.M - 1);
+          src = Ag[q] + (size_t)gr * p.lda * 2 + kb + 16 * (pch ^ swz(r));
+        }
         __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(st + q * A_BYTES + pc * 1024), 16, 0, 0);
       }
 #pragma unroll
@@ -644,6 +704,32 @@ void launch_tile16(const GemmParams& p, hipStream_t s) {
 #undef MOCR_G16
 }
 
+// Implicit-GEMM convolutions (ResNet18 3x3 / 1x1): the ring kernel with the conv A
+// loader; Cout = 64 uses a 128 x 64 tile.
+template <int TM, int TN, int PASSES>
+void launch_conv_tile(const GemmParams& p, hipStream_t s) {
+  constexpr int BM = 16 * TM * 2, BN = 16 * TN * 2;
+  const dim3 grid((p.N / BN) * ((p.M + BM - 1) / BM));
+  switch (p.epi) {
+    case EPI_STORE: gemm_bf16_ring_kernel<TM, TN, 2, 2, EPI_STORE, PASSES, 2, true><<<grid, 256, 0, s>>>(p); break;
+    case EPI_RELU: gemm_bf16_ring_kernel<TM, TN, 2, 2, EPI_RELU, PASSES, 2, true><<<grid, 256, 0, s>>>(p); break;
+    case EPI_RESRELU:
+      gemm_bf16_ring_kernel<TM, TN, 2, 2, EPI_RESRELU, PASSES, 2, true><<<grid, 256, 0, s>>>(p);
+      break;
+    default: throw std::runtime_error("conv: epilogue must be STORE, RELU or RESRELU");
+  }
+}
+
+template <int PASSES>
+void launch_conv_passes(const GemmParams& p, hipStream_t s) {
+  if (p.N % 128 == 0)
+    launch_conv_tile<4, 4, PASSES>(p, s);
+  else if (p.N % 64 == 0)
+    launch_conv_tile<4, 2, PASSES>(p, s);
+  else
+    throw std::runtime_error("conv: Cout must be a multiple of 64");
+}
+
 template <int PASSES>
 void launch_bf16_passes(const GemmParams& p, hipStream_t s) {
   // MOCR_GEMM_RING = 0 (register staging) | 2 | 3 (LDS-DMA ring depth); A/B switch
@@ -672,7 +758,15 @@ void launch_bf16_passes(const GemmParams& p, hipStream_t s) {
 void launch_gemm_bf16(const GemmParams& p, hipStream_t s) {
   if (p.K % BK16 != 0) throw std::runtime_error("gemm_bf16: K must be a multiple of 32");
   if (p.M <= 0) return;
-  if (p.A_lo && p.W_lo) {
+  if (p.conv.on) {
+    const ConvGeom& g = p.conv;
+    if (g.Cin % BK16 != 0 || p.K != g.ks * g.ks * g.Cin || p.M % (g.Hout * g.Wout) != 0 || !p.zero)
+      throw std::runtime_error("conv: geometry does not match the GEMM");
+    if (p.A_lo && p.W_lo)
+      launch_conv_passes<3>(p, s);
+    else
+      launch_conv_passes<1>(p, s);
+  } else if (p.A_lo && p.W_lo) {
     launch_bf16_passes<3>(p, s);
   } else {
     launch_bf16_passes<1>(p, s);

@@ -16,6 +16,17 @@ enum Epi : int {
   EPI_RESADD = 2,  // C += acc + bias                 (x = x + mlp(...), torchvision block)
   EPI_WINRES = 3,  // X[b, y, x] += acc + bias, row m in shifted-window order (window reverse,
                    // roll(+s), crop)  (torchvision shifted_window_attention tail)
+  EPI_RELU = 4,    // C = relu(acc + bias)            (conv + folded BN + ReLU, ResNet BasicBlock)
+  EPI_RESRELU = 5, // C = relu(C + (acc + bias))      (BasicBlock: out += identity; relu)
+};
+
+// Implicit-GEMM convolution (gemm_bf16 only): A row m = output pixel (b, oy, ox) of an
+// NHWC [B, Hin, Win, Cin] input, k = (ky, kx, cin) with cin fastest (Cin % 32 == 0), so
+// a 32-deep k-tile is 64 contiguous bytes of one input pixel; taps outside the map read
+// `zero`.  W is [Cout][ks][ks][Cin].
+struct ConvGeom {
+  int on;
+  int Hin, Win, Cin, Hout, Wout, ks, stride, pad;
 };
 
 struct WinGeom {
@@ -41,10 +52,21 @@ struct GemmParams {
   WinGeom win;
   int col_split;       // EPI_STORE: column block width of a split layout (0 = plain [M, ldc])
   size_t split_stride; // floats between column blocks: C[col/cs][row][col%cs]
+  ConvGeom conv;       // conv.on: A is the implicit im2col of an NHWC map (bf16 planes)
+  const void* zero;    // >= 64 zero bytes (conv padding taps)
 };
 
 void launch_gemm_f32(const GemmParams& p, hipStream_t s);
 void launch_gemm_bf16(const GemmParams& p, hipStream_t s);
+
+// ------------------------------------------------------------------ ResNet18 pieces
+// conv1 7x7/2 (BN folded, w [64][49]) + ReLU + maxpool 3x3/2 -> X [B, H/4, W/4, 64].
+void launch_res_stem(const float* img, const float* w, const float* bias, float* X, uint16_t* Xh, uint16_t* Xl, int B,
+                     int H, int W, hipStream_t s);
+// AdaptiveAvgPool2d((1, None)): NHWC [B, h, w, C] -> [B*w, C].
+void launch_res_avgpool(const float* X, float* P, int B, int h, int w, int C, hipStream_t s);
+// out[r] = pos[r % M] for r < rows (the per-forward positional table, per image).
+void launch_res_posrep(const float* pos, float* out, int rows, int M, int d, hipStream_t s);
 
 // ------------------------------------------------------------------ Swin pieces
 // Stem: Conv2d(1,96,4,4,bias) + Permute + LayerNorm(96) -> X [B, H/4, W/4, 96].
@@ -166,9 +188,13 @@ struct BeamParams {
 void launch_beam_init(const BeamParams& p, hipStream_t s);
 void launch_beam_select(const BeamParams& p, hipStream_t s);
 
+// out[r] = LayerNorm(y[r]) from slice statistics [rows][16][2] (d = 256).
+void launch_ln_rows(const float* y, const float* stats, const float* g, const float* b, float* out, int rows,
+                    hipStream_t s);
+
 void launch_dec_attn(const DecodeState* st, int t, const float* q, const float* K, const float* V,
                      size_t kv_b_stride, int kv_row_stride, int n_fixed, int n_max, float* out, int B, int d,
-                     int heads, hipStream_t s);
+                     int heads, hipStream_t s, int q_ld = 0, int kv_mod = 0);
 
 // Argmax + log-prob + finish flags + next fed token + next step's embedding.
 void launch_dec_argmax(DecodeState* st, int t, int last_step, const float* logits, size_t hist_stride, int ldl,

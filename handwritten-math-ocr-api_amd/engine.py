@@ -22,13 +22,14 @@ LIB_PATH = os.path.join(_HERE, "lib", "libmathocr.so")
 
 PRECISION = {"fp32": 0, "bf16": 1, "bf16x3": 2}
 STOP = {"batch": 0, "none": 1}
-ABI_VERSION = 2
+ARCH = {"swin": 0, "res18trans": 1}
+ABI_VERSION = 3
 
 
 class MocrConfig(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "img_h", "img_w", "vocab", "d_model", "n_heads", "d_ff", "n_layers", "max_pos",
-        "sos_id", "eos_id", "pad_id", "max_batch", "precision", "max_beam")]
+        "sos_id", "eos_id", "pad_id", "max_batch", "precision", "max_beam", "arch")]
 
 
 class KernelStat(ctypes.Structure):
@@ -66,6 +67,7 @@ def load_library(path: str = LIB_PATH):
         "mocr_decode": (I, [P, I, I, i32p, i32p, i32p, f32p, f32p]),
         "mocr_decode_device": (I, [P, I, I, P, i32p]),
         "mocr_decode_beam": (I, [P, I, I, I, i32p, f32p, i32p, i32p]),
+        "mocr_set_encoder_pos": (I, [P, f32p, I]),
         "mocr_debug_encode_until": (I, [P, I, I, f32p, SZ]),
         "mocr_set_timing": (I, [P, I]),
         "mocr_get_timing": (I, [P, ctypes.POINTER(KernelStat), I]),
@@ -84,14 +86,15 @@ def exported_symbols():
     return ["mocr_abi_version", "mocr_weight_count", "mocr_memory_tokens", "mocr_create", "mocr_destroy",
             "mocr_last_error", "mocr_load_weights", "mocr_set_images", "mocr_set_images_device", "mocr_encode",
             "mocr_get_memory", "mocr_decode", "mocr_decode_device", "mocr_decode_beam", "mocr_debug_encode_until",
-            "mocr_set_timing", "mocr_get_timing"]
+            "mocr_set_timing", "mocr_get_timing", "mocr_set_encoder_pos"]
 
 
 def make_config(img_hw=(96, 320), vocab=synth.VOCAB, max_batch=64, precision="fp32", n_layers=synth.N_LAYERS,
-                max_pos=synth.MAX_POS, sos=synth.SOS_ID, eos=synth.EOS_ID, pad=synth.PAD_ID, max_beam=0) -> MocrConfig:
+                max_pos=synth.MAX_POS, sos=synth.SOS_ID, eos=synth.EOS_ID, pad=synth.PAD_ID, max_beam=0,
+                arch="swin") -> MocrConfig:
     return MocrConfig(img_h=img_hw[0], img_w=img_hw[1], vocab=vocab, d_model=synth.D_MODEL, n_heads=synth.N_HEADS,
                       d_ff=synth.D_FF, n_layers=n_layers, max_pos=max_pos, sos_id=sos, eos_id=eos, pad_id=pad,
-                      max_batch=max_batch, precision=PRECISION[precision], max_beam=max_beam)
+                      max_batch=max_batch, precision=PRECISION[precision], max_beam=max_beam, arch=ARCH[arch])
 
 
 def _f32p(a):
@@ -127,10 +130,11 @@ class Engine:
 
     def __init__(self, img_hw=(96, 320), vocab=synth.VOCAB, max_batch=64, precision="fp32", device=0,
                  n_layers=synth.N_LAYERS, max_pos=synth.MAX_POS, sos=synth.SOS_ID, eos=synth.EOS_ID,
-                 pad=synth.PAD_ID, max_beam=0):
+                 pad=synth.PAD_ID, max_beam=0, arch="swin"):
         self.lib = load_library()
-        self.cfg = make_config(img_hw, vocab, max_batch, precision, n_layers, max_pos, sos, eos, pad, max_beam)
+        self.cfg = make_config(img_hw, vocab, max_batch, precision, n_layers, max_pos, sos, eos, pad, max_beam, arch)
         self.max_beam = max_beam
+        self.arch = arch
         self.img_hw = tuple(img_hw)
         self.vocab = vocab
         self.max_batch = max_batch
@@ -172,7 +176,7 @@ class Engine:
         reference key names (see ``weights.pack_state_dict``)."""
         from .weights import pack_state_dict
         blob = weights if isinstance(weights, np.ndarray) and weights.ndim == 1 else pack_state_dict(
-            weights, vocab=self.vocab, max_pos=self.max_pos, n_layers=self.n_layers)
+            weights, vocab=self.vocab, max_pos=self.max_pos, n_layers=self.n_layers, arch=self.arch)
         blob = np.ascontiguousarray(blob, dtype=np.float32)
         self._check(self.lib.mocr_load_weights(self._h, _f32p(blob), blob.size), "mocr_load_weights")
 
@@ -195,6 +199,15 @@ class Engine:
             B = a.shape[0]
             self._check(self.lib.mocr_set_images(self._h, _f32p(a), B), "mocr_set_images")
         self.batch = B
+
+    def set_encoder_pos(self, table):
+        """ResNet18-trans: the positional table [M, 256] the encoder adds after the
+        projection (drawn fresh per forward by the reference, src/model_res18trans.py:57-59;
+        ``synth.make_pos_table(seed, M)`` is torch's draw after ``torch.manual_seed(seed)``)."""
+        t = np.ascontiguousarray(table, dtype=np.float32)
+        if t.shape != (self.memory_tokens, synth.D_MODEL):
+            raise ValueError(f"positional table must be [{self.memory_tokens}, {synth.D_MODEL}], got {list(t.shape)}")
+        self._check(self.lib.mocr_set_encoder_pos(self._h, _f32p(t), t.shape[0]), "mocr_set_encoder_pos")
 
     def _shape_check(self, shape):
         if len(shape) != 4 or shape[1] != 1 or tuple(shape[2:]) != self.img_hw:

@@ -23,13 +23,20 @@ def _to_numpy(v):
     return np.asarray(v, dtype=np.float32)
 
 
-def pack_state_dict(sd, vocab=None, max_pos=None, n_layers=synth.N_LAYERS) -> np.ndarray:
+def detect_arch(sd) -> str:
+    """``res18trans`` for a src/model_res18trans.py state dict, else ``swin``."""
+    return "res18trans" if any(k.startswith("encoder.transformer_encoder.") for k in sd) else "swin"
+
+
+def pack_state_dict(sd, vocab=None, max_pos=None, n_layers=synth.N_LAYERS, arch=None) -> np.ndarray:
     if vocab is None:
         vocab = int(_to_numpy(sd["decoder.fc_out.weight"]).shape[0])
     if max_pos is None:
         max_pos = int(_to_numpy(sd["decoder.pos_encoder.weight"]).shape[0])
+    arch = arch or detect_arch(sd)
+    specs = synth.param_specs(vocab, max_pos, n_layers) if arch == "swin" else synth.param_specs_res18(vocab, max_pos)
     parts = []
-    for name, shape, _, _ in synth.param_specs(vocab, max_pos, n_layers):
+    for name, shape, _, _ in specs:
         key = name
         if key not in sd and name.startswith("encoder.features."):
             key = "encoder.swin." + name[len("encoder."):]

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MOCR_ABI_VERSION 2
+#define MOCR_ABI_VERSION 3
 
 /* Arithmetic of the engine. */
 enum {
@@ -48,6 +48,16 @@ enum {
                              /* relative memory error, NOT token-exact                                */
   MOCR_PRECISION_BF16X3 = 2  /* encoder GEMMs on bf16 MFMA with split operands x = hi + lo,            */
                              /* hi*hi + hi*lo + lo*hi (~1e-5 relative); decoder fp32                  */
+};
+
+/* Model family (the Swin path, and the f3 ResNet18 + Transformer-encoder
+ * variant of src/model_res18trans.py, BASELINE config 5). */
+enum {
+  MOCR_ARCH_SWIN = 0,       /* src/model_swin.py: Swin-T encoder, memory = (H/32 x W/32) tokens        */
+  MOCR_ARCH_RES18TRANS = 1  /* src/model_res18trans.py: ResNet18 (eval BN) + 8 post-norm encoder layers */
+                            /* whose attention runs across the batch (:61-62), memory = W/32 tokens;   */
+                            /* its per-forward random positional table is an input                     */
+                            /* (mocr_set_encoder_pos); convs run bf16x3 (bf16 with MOCR_PRECISION_BF16)  */
 };
 
 /* Greedy stopping rule (src/inference.py:23-25). */
@@ -68,6 +78,7 @@ typedef struct mocr_config {
   int32_t max_batch;     /* device buffers are sized for this many images                          */
   int32_t precision;     /* MOCR_PRECISION_*                                                       */
   int32_t max_beam;      /* 0: greedy only; K <= 8: decoder buffers for max_batch*K hypotheses      */
+  int32_t arch;          /* MOCR_ARCH_*                                                            */
 } mocr_config;
 
 typedef struct mocr_engine mocr_engine;
@@ -95,6 +106,11 @@ int mocr_load_weights(mocr_engine* eng, const float* blob, size_t n_floats);
 /* Images [B,1,H,W] fp32 NCHW in [-1,1] (app/src/preprocess.py:6-17) -> engine buffer. */
 int mocr_set_images(mocr_engine* eng, const float* img_host, int batch);
 int mocr_set_images_device(mocr_engine* eng, const float* img_dev, int batch);
+
+/* MOCR_ARCH_RES18TRANS: the positional table [M, d_model] the encoder adds after the
+ * projection.  The reference draws it fresh in every forward (nn.Embedding(M, d) inside
+ * EncoderCNN.forward, src/model_res18trans.py:57-59); the caller supplies the draw. */
+int mocr_set_encoder_pos(mocr_engine* eng, const float* table, int tokens);
 
 /* Encoder on the resident images: memory [B, M, d_model] and every layer's
  * cross-attention K/V (computed once, not per step as in the reference). */
