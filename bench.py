@@ -49,7 +49,14 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=32, help="images in the CPU-baseline sample")
     ap.add_argument("--no-isolated", dest="isolated", action="store_false", default=True,
                     help="skip the single-replica latency / roofline pass")
-    return ap.parse_args()
+    ap.add_argument("--arch", default="swin", choices=["swin", "res18trans"],
+                    help="res18trans: BASELINE config 5 (src/model_res18trans.py)")
+    ap.add_argument("--beam", type=int, default=0,
+                    help="K > 0: beam search (BASELINE config 4: --beam 4 --batch 32 --tokens 256)")
+    a = ap.parse_args()
+    if a.beam and a.arch != "swin":
+        ap.error("--beam is measured on the Swin path")
+    return a
 
 
 def cpu_baseline(args, pkg):
@@ -84,7 +91,8 @@ def pmc_traffic(precision, cls):
 def roofline(stats, dtype, precision):
     """Dominant encoder GEMM class by event-timed GPU time: algorithmic FLOP per launch /
     average launch duration, against the dense MFMA peak of the arithmetic."""
-    gemms = {k: v for k, v in stats.items() if v["flops"] > 0 and "attn" not in k and k != "stem"}
+    gemms = {k: v for k, v in stats.items()
+             if v["flops"] > 0 and "attn" not in k and not k.endswith("stem") and k != "r.enc"}
     name, d = max(gemms.items(), key=lambda kv: kv[1]["total_ms"])
     avg_ms = d["total_ms"] / d["launches"]
     flops = d["flops"] / d["launches"]
@@ -111,18 +119,30 @@ def main():
     B, S, R = args.batch, args.tokens, args.replicas
     dtype = DTYPE[args.precision]
 
-    pool = pkg.pipeline.ReplicaPool(R, img_hw=(H, W), max_batch=B, precision=args.precision, device=local)
-    pool.load_weights(pkg.synth.make_weights(1234, "init"))
-    # each replica holds its own 64-image batch of this rank's shard, resident in HBM
+    # 256 beam-search tokens need a positional table of >= 257 rows (the reference's has 150,
+    # src/model_swin.py:54): synthetic weights with 260 rows for that config
+    max_pos = max(pkg.synth.MAX_POS, S + 4) if args.beam else pkg.synth.MAX_POS
+    ekw = dict(img_hw=(H, W), max_batch=B, precision=args.precision, device=local, arch=args.arch,
+               max_beam=args.beam, max_pos=max_pos)
+    pool = pkg.pipeline.ReplicaPool(R, **ekw)
+    weights = pkg.synth.make_weights(1234, "init", arch=args.arch, max_pos=max_pos)
+    pool.load_weights(weights)
+    # each replica holds its own batch of this rank's shard, resident in HBM
     for i, e in enumerate(pool.engines):
         seed0 = 1000 + (rank * R + i) * B
         e.set_images(torch.from_numpy(pkg.synth.make_images(B, H, W, seed0=seed0)).to(dev))
+        if args.arch == "res18trans":
+            e.set_encoder_pos(pkg.synth.make_pos_table(5, e.memory_tokens))
 
     def step(eng, _k):
         t0 = time.perf_counter()
         ids = torch.empty((B, S + 1), dtype=torch.int32, device=dev)
         eng.encode()
-        eng.decode_into(ids, max_steps=S, stop="none")
+        if args.beam:
+            r = eng.beam_search(beam=args.beam, max_steps=S, stop="none")
+            ids.copy_(torch.from_numpy(r.ids))
+        else:
+            eng.decode_into(ids, max_steps=S, stop="none")
         return ids, time.perf_counter() - t0
 
     def run(n):
@@ -158,14 +178,19 @@ def main():
             ts.append(dt)
         stats = e.timing()
         e.set_timing(False)
-        e1 = pkg.Engine(img_hw=(H, W), max_batch=1, precision=args.precision, device=local)
-        e1.load_weights(pkg.synth.make_weights(1234, "init"))
+        e1 = pkg.Engine(**dict(ekw, max_batch=1))
+        e1.load_weights(weights)
         e1.set_images(torch.from_numpy(pkg.synth.make_images(1, H, W, seed0=1000)).to(dev))
+        if args.arch == "res18trans":
+            e1.set_encoder_pos(pkg.synth.make_pos_table(5, e1.memory_tokens))
         t1s = []
         for _ in range(3):
             t1 = time.perf_counter()
             e1.encode()
-            e1.decode(max_steps=S, stop="none")
+            if args.beam:
+                e1.beam_search(beam=args.beam, max_steps=S, stop="none")
+            else:
+                e1.decode(max_steps=S, stop="none")
             t1s.append(time.perf_counter() - t1)
         e1.close()
         iso = {"batch_latency_ms": statistics.median(ts) * 1e3, "b1_latency_ms": statistics.median(t1s) * 1e3,
@@ -189,9 +214,14 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": dtype,
-        "data": "synthetic: U(-1,1) 384x384x1 images (PCG64 seeds 1000+i), random-init weights with the "
-                "reference's init distributions (seed 1234); 128 greedy steps, no early stop",
-        "config": {"workload": f"B{B} {H}x{W} Swin-T + 8L decoder greedy@{S}, per GPU", "global_batch": world * B,
+        "data": f"synthetic: U(-1,1) {H}x{W}x1 images (PCG64 seeds 1000+i), random-init weights with the "
+                f"reference's init distributions (seed 1234"
+                + (f", positional table of {max_pos} rows" if args.beam else "")
+                + (", encoder positional table torch seed 5" if args.arch == "res18trans" else "")
+                + f"); {S} {'beam-' + str(args.beam) if args.beam else 'greedy'} steps, no early stop",
+        "config": {"workload": f"B{B} {H}x{W} {'Swin-T' if args.arch == 'swin' else 'ResNet18+8L-enc'} + 8L decoder "
+                               f"{'beam' + str(args.beam) if args.beam else 'greedy'}@{S}, per GPU",
+                   "global_batch": world * B,
                    "per_gpu_batch": B, "image": [H, W], "max_tokens": S, "vocab": pkg.synth.VOCAB,
                    "decoder_layers": pkg.synth.N_LAYERS, "parallelism": f"image-parallel x{world}",
                    "replicas_per_gpu": R, "precision": args.precision},
@@ -205,7 +235,7 @@ def main():
         out["kernel_classes"] = {k: {"launches": v["launches"], "avg_ms": v["total_ms"] / v["launches"],
                                      "tflops": v["flops"] / v["total_ms"] * 1e-9 if v["total_ms"] else None}
                                  for k, v in sorted(iso["stats"].items())}
-    if args.cpu_baseline and world == 1:
+    if args.cpu_baseline and world == 1 and args.arch == "swin" and not args.beam:
         out["cpu_baseline"] = cpu_baseline(args, pkg)
     pool.close()
     print(json.dumps(out))

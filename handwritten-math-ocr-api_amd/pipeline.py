@@ -4,8 +4,9 @@ A greedy decode step is a chain of small, latency-bound kernels that leaves most
 idle, while the encoder is a throughput-bound stream of large GEMMs.  Batches are
 independent, so R engines on the same device, each driven by its own thread (ctypes
 releases the GIL; each engine has its own HIP stream), overlap one batch's decode
-with another batch's encoder.  Measured at B=64, 384², bf16x3: 1 replica 888 img/s,
-2 → 1296, 3 → 1509, 4 → 1305 (more streams than the 4 hardware queues).
+with another batch's encoder.  GPU time adds up: at B=64, 384², bf16x3, 3 replicas,
+encode-only 5263 img/s and decode-only 3250 img/s give 1998 img/s together
+(tools/pipeline_probe.py); 1 → 1146, 2 → 1681, 3 → 2003, 4 → 2210 img/s (bench.py).
 
 ``imap`` preserves submission order, so callers can run an order-sensitive step
 (e.g. the RCCL gather of token streams in ``bench.py``) on the results, identically on
@@ -35,7 +36,7 @@ class ReplicaPool:
         from .weights import pack_state_dict
         e0 = self.engines[0]
         blob = weights if hasattr(weights, "ndim") and weights.ndim == 1 else pack_state_dict(
-            weights, vocab=e0.vocab, max_pos=e0.max_pos, n_layers=e0.n_layers)
+            weights, vocab=e0.vocab, max_pos=e0.max_pos, n_layers=e0.n_layers, arch=e0.arch)
         for e in self.engines:
             e.load_weights(blob)
 
