@@ -19,30 +19,6 @@ __device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
   return (uint16_t)(u >> 16);
 }
 
-// LayerNorm of one row held as NPER values per lane (element c = lane + 64*i), C valid.
-template <int NPER>
-__device__ __forceinline__ void ln_regs(float (&v)[NPER], int C, int lane, const float* g, const float* b) {
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < NPER; ++i)
-    if (lane + 64 * i < C) s += v[i];
-  const float mean = wave_sum(s) / (float)C;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < NPER; ++i)
-    if (lane + 64 * i < C) {
-      const float d = v[i] - mean;
-      q += d * d;
-    }
-  const float var = wave_sum(q) / (float)C;
-  const float rstd = 1.0f / sqrtf(var + 1e-5f);
-#pragma unroll
-  for (int i = 0; i < NPER; ++i) {
-    const int c = lane + 64 * i;
-    if (c < C) v[i] = (v[i] - mean) * rstd * g[c] + b[c];
-  }
-}
-
 // Row outputs: fp32 and/or bf16 hi plane and/or lo plane (x - bf16(x)), as the
 // consuming GEMM's precision needs.
 struct RowOut {
@@ -60,133 +36,203 @@ __device__ __forceinline__ void store_val(const RowOut& o, size_t off, float v) 
   }
 }
 
-template <int NPER>
-__device__ __forceinline__ void store_row(float (&v)[NPER], int C, int lane, const RowOut& o, size_t row_off) {
-#pragma unroll
-  for (int i = 0; i < NPER; ++i) {
-    const int c = lane + 64 * i;
-    if (c < C) store_val(o, row_off + c, v[i]);
-  }
-}
+// ---------------------------------------------------------------- row-group LayerNorm
+// LPR lanes per row, F floats per lane (C = LPR*F: 96 -> 8 lanes, 192 -> 16, 384 -> 32,
+// 768 -> 64 with F = 12; 1536 -> 64 with F = 24), 16-B loads and stores, statistics
+// reduced over the row's lanes with shuffles (mean, then Σ(x - mean)², two passes).
+//   MODE_ROWS:  Y[r] = LN(X[r]);
+//   MODE_WIN:   row r of the shifted-window partition (ln_partition_kernel's mapping;
+//               padded tokens are zero rows);
+//   MODE_MERGE: PatchMerging's [x(0,0), x(1,0), x(0,1), x(1,1)] gather (merge_ln_kernel).
+enum { MODE_ROWS = 0, MODE_WIN = 1, MODE_MERGE = 2 };
 
-// ---------------------------------------------------------------------------- stem
-// Conv2d(1, 96, k=4, s=4, bias) -> Permute -> LayerNorm(96).  One wave per output token.
-__global__ void __launch_bounds__(256) stem_kernel(const float* __restrict__ img, const float* __restrict__ w,
-                                                   const float* __restrict__ bias, const float* __restrict__ g,
-                                                   const float* __restrict__ beta, float* __restrict__ X, int B,
-                                                   int H, int W, int Hs, int Ws) {
-  const int lane = threadIdx.x & 63;
-  const long tok = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (tok >= (long)B * Hs * Ws) return;
-  const int b = (int)(tok / (Hs * Ws));
-  const int rem = (int)(tok - (long)b * Hs * Ws);
-  const int y = rem / Ws;
-  const int x = rem - y * Ws;
-  float px[16];
-  const float* src = img + ((size_t)b * H + 4 * y) * W + 4 * x;
-#pragma unroll
-  for (int ky = 0; ky < 4; ++ky)
-#pragma unroll
-    for (int kx = 0; kx < 4; ++kx) px[ky * 4 + kx] = src[(size_t)ky * W + kx];
-  float v[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int c = lane + 64 * i;
-    float acc = 0.f;
-    if (c < 96) {
-      const float* wc = w + c * 16;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) acc = fmaf(wc[k], px[k], acc);
-      acc += bias[c];
-    }
-    v[i] = acc;
-  }
-  ln_regs<2>(v, 96, lane, g, beta);
-  store_row<2>(v, 96, lane, RowOut{X, nullptr, nullptr}, (size_t)tok * 96);
-}
+struct LnGeom {
+  long rows;
+  int C;         // row length (4C for MODE_MERGE)
+  int B, H, W;   // MODE_MERGE: input map; MODE_WIN: via win
+  int Cin;       // MODE_MERGE: input channels
+  WinGeom win;
+};
 
-// ---------------------------------------------------------------- LN + window partition
-template <int NPER>
-__global__ void __launch_bounds__(256) ln_partition_kernel(const float* __restrict__ X, const float* __restrict__ g,
-                                                           const float* __restrict__ b, RowOut out, int B, int C,
-                                                           WinGeom wg) {
+template <int LPR, int F, int MODE>
+__global__ void __launch_bounds__(256) ln_group_kernel(const float* __restrict__ X, const float* __restrict__ g,
+                                                       const float* __restrict__ b, RowOut out, LnGeom geo) {
+  constexpr int RPW = 64 / LPR;
   const int lane = threadIdx.x & 63;
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int per_img = wg.nWin * kWinTok;
-  if (row >= (long)B * per_img) return;
-  const int bi = (int)(row / per_img);
-  const int rem = (int)(row - (long)bi * per_img);
-  const int win = rem / kWinTok;
-  const int tk = rem - win * kWinTok;
-  const int wy = win / wg.nWx;
-  const int wx = win - wy * wg.nWx;
-  int y = wy * kWin + tk / kWin + wg.sh;
-  int x = wx * kWin + tk % kWin + wg.sw;
-  if (y >= wg.pH) y -= wg.pH;
-  if (x >= wg.pW) x -= wg.pW;
-  float v[NPER];
-  if (y < wg.H && x < wg.W) {
-    const float* src = X + ((size_t)(bi * wg.H + y) * wg.W + x) * C;
+  const int gi = lane % LPR;
+  const long row = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  const bool live = row < geo.rows;
+  const int c0 = gi * F;
+  float v[F];
 #pragma unroll
-    for (int i = 0; i < NPER; ++i) {
-      const int c = lane + 64 * i;
-      v[i] = c < C ? src[c] : 0.f;
-    }
-    ln_regs<NPER>(v, C, lane, g, b);
-  } else {
-#pragma unroll
-    for (int i = 0; i < NPER; ++i) v[i] = 0.f;  // F.pad after norm1: zero tokens
-  }
-  store_row<NPER>(v, C, lane, out, (size_t)row * C);
-}
-
-template <int NPER>
-__global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict__ X, const float* __restrict__ g,
-                                                        const float* __restrict__ b, RowOut out, long rows, int C) {
-  const int lane = threadIdx.x & 63;
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const float* src = X + (size_t)row * C;
-  float v[NPER];
-#pragma unroll
-  for (int i = 0; i < NPER; ++i) {
-    const int c = lane + 64 * i;
-    v[i] = c < C ? src[c] : 0.f;
-  }
-  ln_regs<NPER>(v, C, lane, g, b);
-  store_row<NPER>(v, C, lane, out, (size_t)row * C);
-}
-
-// ---------------------------------------------------------------- PatchMerging + LN(4C)
-template <int NPER>
-__global__ void __launch_bounds__(256) merge_ln_kernel(const float* __restrict__ X, const float* __restrict__ g,
-                                                       const float* __restrict__ b, RowOut out, int B, int H, int W,
-                                                       int C) {
-  const int lane = threadIdx.x & 63;
-  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= (long)B * Ho * Wo) return;
-  const int bi = (int)(row / (Ho * Wo));
-  const int rem = (int)(row - (long)bi * Ho * Wo);
-  const int oy = rem / Wo;
-  const int ox = rem - oy * Wo;
-  const int C4 = 4 * C;
-  float v[NPER];
-#pragma unroll
-  for (int i = 0; i < NPER; ++i) {
-    const int c4 = lane + 64 * i;
-    float val = 0.f;
-    if (c4 < C4) {
-      const int q = c4 / C;          // cat order x0=(0,0), x1=(1,0), x2=(0,1), x3=(1,1) as (dy,dx)
-      const int c = c4 - q * C;
+  for (int e = 0; e < F; ++e) v[e] = 0.f;
+  bool zero_row = !live;
+  const float* src = nullptr;
+  if (live) {
+    if constexpr (MODE == MODE_ROWS) {
+      src = X + (size_t)row * geo.C + c0;
+    } else if constexpr (MODE == MODE_WIN) {
+      const WinGeom& wg = geo.win;
+      const int per_img = wg.nWin * kWinTok;
+      const int bi = (int)(row / per_img);
+      const int rem = (int)(row - (long)bi * per_img);
+      const int win = rem / kWinTok;
+      const int tk = rem - win * kWinTok;
+      const int wy = win / wg.nWx;
+      const int wx = win - wy * wg.nWx;
+      int y = wy * kWin + tk / kWin + wg.sh;
+      int x = wx * kWin + tk % kWin + wg.sw;
+      if (y >= wg.pH) y -= wg.pH;
+      if (x >= wg.pW) x -= wg.pW;
+      if (y < wg.H && x < wg.W) src = X + ((size_t)(bi * wg.H + y) * wg.W + x) * geo.C + c0;
+      else zero_row = true;  // F.pad after norm1: zero token, LayerNorm not applied
+    } else {
+      const int Ho = (geo.H + 1) / 2, Wo = (geo.W + 1) / 2;
+      const int bi = (int)(row / ((long)Ho * Wo));
+      const int rem = (int)(row - (long)bi * Ho * Wo);
+      const int oy = rem / Wo;
+      const int ox = rem - oy * Wo;
+      const int q = c0 / geo.Cin;  // cat order (dy,dx) = (0,0), (1,0), (0,1), (1,1)
       const int y = 2 * oy + (q & 1);
       const int x = 2 * ox + (q >> 1);
-      if (y < H && x < W) val = X[((size_t)(bi * H + y) * W + x) * C + c];
+      if (y < geo.H && x < geo.W) src = X + ((size_t)(bi * geo.H + y) * geo.W + x) * geo.Cin + (c0 - q * geo.Cin);
     }
-    v[i] = val;
   }
-  ln_regs<NPER>(v, C4, lane, g, b);
-  store_row<NPER>(v, C4, lane, out, (size_t)row * C4);
+  if (src) {
+#pragma unroll
+    for (int e = 0; e < F; e += 4) {
+      const floatx4 t = *reinterpret_cast<const floatx4*>(src + e);
+      v[e] = t[0];
+      v[e + 1] = t[1];
+      v[e + 2] = t[2];
+      v[e + 3] = t[3];
+    }
+  }
+  if (!zero_row) {
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < F; ++e) s += v[e];
+#pragma unroll
+    for (int m = 1; m < LPR; m <<= 1) s += __shfl_xor(s, m, 64);
+    const float mean = s / (float)geo.C;
+    float q = 0.f;
+#pragma unroll
+    for (int e = 0; e < F; ++e) {
+      const float d = v[e] - mean;
+      q += d * d;
+    }
+#pragma unroll
+    for (int m = 1; m < LPR; m <<= 1) q += __shfl_xor(q, m, 64);
+    const float rstd = 1.0f / sqrtf(q / (float)geo.C + 1e-5f);
+#pragma unroll
+    for (int e = 0; e < F; e += 4) {
+      const floatx4 gg = *reinterpret_cast<const floatx4*>(g + c0 + e);
+      const floatx4 bb = *reinterpret_cast<const floatx4*>(b + c0 + e);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[e + k] = (v[e + k] - mean) * rstd * gg[k] + bb[k];
+    }
+  }
+  if (!live) return;
+  const size_t off = (size_t)row * geo.C + c0;
+#pragma unroll
+  for (int e = 0; e < F; e += 4) {
+    if (out.f32) *reinterpret_cast<floatx4*>(out.f32 + off + e) = floatx4{v[e], v[e + 1], v[e + 2], v[e + 3]};
+    if (out.hi) {
+      uint16_t h[4], l[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        h[k] = f32_to_bf16_rne(v[e + k]);
+        l[k] = f32_to_bf16_rne(v[e + k] - __uint_as_float((uint32_t)h[k] << 16));
+      }
+      *reinterpret_cast<uint2*>(out.hi + off + e) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+      if (out.lo)
+        *reinterpret_cast<uint2*>(out.lo + off + e) =
+            make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+    }
+  }
+}
+
+template <int MODE>
+void launch_ln_group(const float* X, const float* g, const float* b, const RowOut& o, const LnGeom& geo,
+                     hipStream_t s) {
+  auto blocks = [&](int lpr) { return (unsigned)((geo.rows + 4 * (64 / lpr) - 1) / (4 * (64 / lpr))); };
+  switch (geo.C) {
+    case 96: ln_group_kernel<8, 12, MODE><<<blocks(8), 256, 0, s>>>(X, g, b, o, geo); break;
+    case 192: ln_group_kernel<16, 12, MODE><<<blocks(16), 256, 0, s>>>(X, g, b, o, geo); break;
+    case 384: ln_group_kernel<32, 12, MODE><<<blocks(32), 256, 0, s>>>(X, g, b, o, geo); break;
+    case 768: ln_group_kernel<64, 12, MODE><<<blocks(64), 256, 0, s>>>(X, g, b, o, geo); break;
+    case 1536: ln_group_kernel<64, 24, MODE><<<blocks(64), 256, 0, s>>>(X, g, b, o, geo); break;
+    default: throw std::runtime_error("layernorm: unsupported row length " + std::to_string(geo.C));
+  }
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------- stem (vectorised)
+// Conv2d(1, 96, 4, 4) + LayerNorm(96): 16 lanes per token, 6 channels per lane whose
+// 6x16 weights stay in registers over a grid-stride loop of tokens; the token's 4x4
+// patch is 4 float4 loads (shared by the 16 lanes); LayerNorm over the 16 lanes.
+__global__ void __launch_bounds__(256) stem16_kernel(const float* __restrict__ img, const float* __restrict__ w,
+                                                     const float* __restrict__ bias, const float* __restrict__ g,
+                                                     const float* __restrict__ beta, float* __restrict__ X, long ntok,
+                                                     int H, int W, int Hs, int Ws) {
+  const int lane = threadIdx.x & 63;
+  const int gi = lane & 15;
+  const int c0 = gi * 6;
+  float wr[6][16], br[6], gr[6], be[6];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) wr[c][k] = w[(c0 + c) * 16 + k];
+    br[c] = bias[c0 + c];
+    gr[c] = g[c0 + c];
+    be[c] = beta[c0 + c];
+  }
+  const long step = (long)gridDim.x * 16;
+  for (long tok = (long)blockIdx.x * 16 + (threadIdx.x >> 4); tok < ntok; tok += step) {
+    const int b = (int)(tok / ((long)Hs * Ws));
+    const int rem = (int)(tok - (long)b * Hs * Ws);
+    const int y = rem / Ws;
+    const int x = rem - y * Ws;
+    const float* src = img + ((size_t)b * H + 4 * y) * W + 4 * x;
+    float px[16];
+#pragma unroll
+    for (int ky = 0; ky < 4; ++ky) {
+      const floatx4 t = *reinterpret_cast<const floatx4*>(src + (size_t)ky * W);
+      px[4 * ky] = t[0];
+      px[4 * ky + 1] = t[1];
+      px[4 * ky + 2] = t[2];
+      px[4 * ky + 3] = t[3];
+    }
+    float v[6];
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc = fmaf(wr[c][k], px[k], acc);
+      v[c] = acc + br[c];
+      s += v[c];
+    }
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) s += __shfl_xor(s, m, 64);
+    const float mean = s / 96.f;
+    float q = 0.f;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      const float d = v[c] - mean;
+      q += d * d;
+    }
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) q += __shfl_xor(q, m, 64);
+    const float rstd = 1.0f / sqrtf(q / 96.f + 1e-5f);
+    float* dst = X + (size_t)tok * 96 + c0;
+    float o[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) o[c] = (v[c] - mean) * rstd * gr[c] + be[c];
+    *reinterpret_cast<float2*>(dst) = make_float2(o[0], o[1]);
+    *reinterpret_cast<float2*>(dst + 2) = make_float2(o[2], o[3]);
+    *reinterpret_cast<float2*>(dst + 4) = make_float2(o[4], o[5]);
+  }
 }
 
 // ---------------------------------------------------------------- window attention
@@ -524,49 +570,40 @@ inline unsigned blocks_for_rows(long rows) { return (unsigned)((rows + 3) / 4); 
 void launch_stem(const float* img, const float* w, const float* b, const float* ln_w, const float* ln_b, float* X,
                  int B, int H, int W, hipStream_t s) {
   const int Hs = H / 4, Ws = W / 4;
-  stem_kernel<<<blocks_for_rows((long)B * Hs * Ws), 256, 0, s>>>(img, w, b, ln_w, ln_b, X, B, H, W, Hs, Ws);
+  if (W % 4 != 0) throw std::runtime_error("stem: image width must be a multiple of 4");
+  const long ntok = (long)B * Hs * Ws;
+  const unsigned blocks = (unsigned)std::min<long>((ntok + 15) / 16, 4096);
+  stem16_kernel<<<blocks, 256, 0, s>>>(img, w, b, ln_w, ln_b, X, ntok, H, W, Hs, Ws);
   MOCR_HIP_CHECK(hipGetLastError());
 }
 
 void launch_ln_partition(const float* X, const float* g, const float* b, float* XW, uint16_t* XWh, uint16_t* XWl,
                          int B, int C, const WinGeom& wg, hipStream_t s) {
-  const long rows = (long)B * wg.nWin * kWinTok;
-  const RowOut o{XW, XWh, XWl};
-  switch ((C + 63) / 64) {
-    case 2: ln_partition_kernel<2><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, B, C, wg); break;
-    case 3: ln_partition_kernel<3><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, B, C, wg); break;
-    case 6: ln_partition_kernel<6><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, B, C, wg); break;
-    case 12: ln_partition_kernel<12><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, B, C, wg); break;
-    default: throw std::runtime_error("ln_partition: unsupported C " + std::to_string(C));
-  }
-  MOCR_HIP_CHECK(hipGetLastError());
+  LnGeom geo{};
+  geo.rows = (long)B * wg.nWin * kWinTok;
+  geo.C = C;
+  geo.win = wg;
+  launch_ln_group<MODE_WIN>(X, g, b, RowOut{XW, XWh, XWl}, geo, s);
 }
 
 void launch_layernorm(const float* X, const float* g, const float* b, float* Y, uint16_t* Yh, uint16_t* Yl,
                       int rows, int C, hipStream_t s) {
-  const RowOut o{Y, Yh, Yl};
-  switch ((C + 63) / 64) {
-    case 2: layernorm_kernel<2><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, rows, C); break;
-    case 3: layernorm_kernel<3><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, rows, C); break;
-    case 4: layernorm_kernel<4><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, rows, C); break;
-    case 6: layernorm_kernel<6><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, rows, C); break;
-    case 12: layernorm_kernel<12><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, rows, C); break;
-    default: throw std::runtime_error("layernorm: unsupported C " + std::to_string(C));
-  }
-  MOCR_HIP_CHECK(hipGetLastError());
+  LnGeom geo{};
+  geo.rows = rows;
+  geo.C = C;
+  launch_ln_group<MODE_ROWS>(X, g, b, RowOut{Y, Yh, Yl}, geo, s);
 }
 
 void launch_merge_ln(const float* X, const float* g, const float* b, float* Y, uint16_t* Yh, uint16_t* Yl, int B,
                      int H, int W, int C, hipStream_t s) {
-  const RowOut o{Y, Yh, Yl};
-  const long rows = (long)B * ((H + 1) / 2) * ((W + 1) / 2);
-  switch ((4 * C + 63) / 64) {
-    case 6: merge_ln_kernel<6><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, B, H, W, C); break;
-    case 12: merge_ln_kernel<12><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, B, H, W, C); break;
-    case 24: merge_ln_kernel<24><<<blocks_for_rows(rows), 256, 0, s>>>(X, g, b, o, B, H, W, C); break;
-    default: throw std::runtime_error("merge_ln: unsupported C " + std::to_string(C));
-  }
-  MOCR_HIP_CHECK(hipGetLastError());
+  LnGeom geo{};
+  geo.rows = (long)B * ((H + 1) / 2) * ((W + 1) / 2);
+  geo.C = 4 * C;
+  geo.B = B;
+  geo.H = H;
+  geo.W = W;
+  geo.Cin = C;
+  launch_ln_group<MODE_MERGE>(X, g, b, RowOut{Y, Yh, Yl}, geo, s);
 }
 
 void launch_window_attention(const float* QKV, const float* relbias, const float* relmask, float* O, uint16_t* Oh,
