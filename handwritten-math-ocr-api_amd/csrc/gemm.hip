@@ -730,10 +730,48 @@ void launch_conv_passes(const GemmParams& p, hipStream_t s) {
     throw std::runtime_error("conv: Cout must be a multiple of 64");
 }
 
+// 256-row tiles: 8 waves as 2 (M) x 4 (N), each 128 x 16*TN, 2-stage ring (bf16x3: 2 x
+// 64 KB of LDS, 1 block per CU).  Half the operand re-reads per MFMA of the 128-row
+// tiles, but one k-tile in flight at one block per CU: measured (B=64, 384²) faster on
+// bf16x3 GEMMs with K <= N (s1.fc1 435 -> 393 us, s2.qkv 212 -> 174, s2.fc1 276 -> 237,
+// s4.qkv 149 -> 136) and slower with K > N (s2.fc2 232 -> 257, s3.fc2 180 -> 191) and in
+// plain bf16.  Used for bf16x3 with K <= N and >= MOCR_GEMM_BIG_MIN tiles (default 384;
+// 0 disables).
+template <int TN, int PASSES>
+void launch_big_tile(const GemmParams& p, hipStream_t s) {
+  constexpr int BM = 256, BN = 64 * TN;
+  const dim3 grid((p.N / BN) * ((p.M + BM - 1) / BM));
+  switch (p.epi) {
+    case EPI_STORE: gemm_bf16_ring_kernel<8, TN, 2, 4, EPI_STORE, PASSES, 2><<<grid, 512, 0, s>>>(p); break;
+    case EPI_GELU: gemm_bf16_ring_kernel<8, TN, 2, 4, EPI_GELU, PASSES, 2><<<grid, 512, 0, s>>>(p); break;
+    case EPI_RESADD: gemm_bf16_ring_kernel<8, TN, 2, 4, EPI_RESADD, PASSES, 2><<<grid, 512, 0, s>>>(p); break;
+    case EPI_WINRES: gemm_bf16_ring_kernel<8, TN, 2, 4, EPI_WINRES, PASSES, 2><<<grid, 512, 0, s>>>(p); break;
+    default: throw std::runtime_error("gemm_bf16: bad epilogue");
+  }
+}
+
+template <int PASSES>
+bool try_big_tile(const GemmParams& p, hipStream_t s) {
+  static const long min_tiles = getenv("MOCR_GEMM_BIG_MIN") ? atol(getenv("MOCR_GEMM_BIG_MIN")) : 384;
+  if (min_tiles <= 0 || PASSES != 3 || p.K > p.N) return false;
+  const long mt = (p.M + 255) / 256;
+  if (p.N % 256 == 0 && mt * (p.N / 256) >= min_tiles) {
+    launch_big_tile<4, PASSES>(p, s);
+  } else if (p.N % 192 == 0 && mt * (p.N / 192) >= min_tiles) {
+    launch_big_tile<3, PASSES>(p, s);
+  } else if (p.N % 128 == 0 && mt * (p.N / 128) >= min_tiles) {
+    launch_big_tile<2, PASSES>(p, s);
+  } else {
+    return false;
+  }
+  return true;
+}
+
 template <int PASSES>
 void launch_bf16_passes(const GemmParams& p, hipStream_t s) {
   // MOCR_GEMM_RING = 0 (register staging) | 2 | 3 (LDS-DMA ring depth); A/B switch
   static const int ring = getenv("MOCR_GEMM_RING") ? atoi(getenv("MOCR_GEMM_RING")) : 2;
+  if (ring == 2 && try_big_tile<PASSES>(p, s)) return;
   if (p.N % 128 == 0) {  // 128 x 128, waves of 64 x 64
     if (ring == 3)
       launch_tile16<4, 4, 2, 2, PASSES, 3>(p, s);
