@@ -29,6 +29,16 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // Exact (erf) GELU, torch.nn.GELU() default: x * 0.5 * (1 + erf(x / sqrt(2))).
+// bf16 hi/lo planes of two floats: hi = bf16(x) (round to nearest even, the hardware
+// v_cvt_pk_bf16_f32), lo = bf16(x - hi).  Packed pairs: element 0 in the low half.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split2_bf16(float a, float b, uint32_t& hi, uint32_t& lo) {
+  const bf16x2_t h = {(__bf16)a, (__bf16)b};
+  hi = __builtin_bit_cast(uint32_t, h);
+  const bf16x2_t l = {(__bf16)(a - __uint_as_float(hi << 16)), (__bf16)(b - __uint_as_float(hi & 0xffff0000u))};
+  lo = __builtin_bit_cast(uint32_t, l);
+}
+
 __device__ __forceinline__ float gelu_erf(float x) {
   return x * 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
 }

@@ -761,7 +761,7 @@ __global__ void __launch_bounds__(256) dec_argmax_kernel(DecodeState* st, int t,
   // one pass: running (max, first argmax, Σ exp(l - max)) per thread, then merged
   float best = -INFINITY, sum = 0.f;
   int bidx = 0x7fffffff;
-  constexpr int CH = 8;  // loads in flight per thread
+  constexpr int CH = 20;  // loads in flight per thread: one round for V <= 5120
   for (int j0 = tid; j0 < V; j0 += 256 * CH) {
     float vals[CH];
 #pragma unroll

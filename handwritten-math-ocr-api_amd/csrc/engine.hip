@@ -89,7 +89,7 @@ struct Layout {
       off += n;
       return o;
     };
-    const size_t d = c.d_model, ff = c.d_ff, V = c.vocab;
+    const size_t d = c.d_model, ff = c.d_ff;
     arch = c.arch;
     if (arch == MOCR_ARCH_RES18TRANS) {
       auto conv = [&](int cin, int cout, int ks, int stride) {

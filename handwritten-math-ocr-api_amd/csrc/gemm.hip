@@ -277,6 +277,20 @@ __device__ __forceinline__ void epi_store16(const GemmParams& p, int row, int co
   }
 }
 
+// GELU for the bf16 / bf16x3 epilogues: erf by Abramowitz & Stegun 7.1.26 (one
+// reciprocal, one exp, 6 FMAs, no branches; |erf error| <= 1.5e-7, two orders below the
+// bf16x3 products' ~1e-5).  The fp32 path keeps the library erff (gelu_erf).
+__device__ __forceinline__ float gelu_fast(float x) {
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __frcp_rn(fmaf(0.3275911f, z, 1.0f));
+  float poly = fmaf(1.061405429f, t, -1.453152027f);
+  poly = fmaf(poly, t, 1.421413741f);
+  poly = fmaf(poly, t, -0.284496736f);
+  poly = fmaf(poly, t, 0.254829592f);
+  const float e = 1.0f - poly * t * __expf(-z * z);  // erf(|x| / sqrt 2)
+  return x * 0.5f * (1.0f + copysignf(e, x));
+}
+
 // Row-vector epilogue: 8 consecutive columns of one output row (col % 8 == 0), the same
 // arithmetic as epi_store/epi_store16 element by element, but 16/32-B loads and stores.
 template <int EPI>
@@ -303,14 +317,12 @@ __device__ __forceinline__ void epi_vec8(const GemmParams& p, int row, int col, 
     *reinterpret_cast<floatx4*>(c) = floatx4{v[0], v[1], v[2], v[3]};
     *reinterpret_cast<floatx4*>(c + 4) = floatx4{v[4], v[5], v[6], v[7]};
     if (p.C16) {
-      u16x8 hi, lo;
+      uint32_t hi[4], lo[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        hi[e] = bf16_rne(v[e]);
-        lo[e] = bf16_rne(v[e] - bf16_to_f32(hi[e]));
-      }
-      *reinterpret_cast<u16x8*>(static_cast<uint16_t*>(p.C16) + off) = hi;
-      if (p.C16lo) *reinterpret_cast<u16x8*>(static_cast<uint16_t*>(p.C16lo) + off) = lo;
+      for (int e = 0; e < 4; ++e) split2_bf16(v[2 * e], v[2 * e + 1], hi[e], lo[e]);
+      *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.C16) + off) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+      if (p.C16lo)
+        *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.C16lo) + off) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
     }
   } else if constexpr (EPI == EPI_RESADD || EPI == EPI_WINRES) {
     float* c;
@@ -344,7 +356,7 @@ __device__ __forceinline__ void epi_vec8(const GemmParams& p, int row, int col, 
   } else {
     if constexpr (EPI == EPI_GELU) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+      for (int e = 0; e < 8; ++e) v[e] = gelu_fast(v[e]);
     }
     if constexpr (EPI == EPI_RELU) {
 #pragma unroll
@@ -361,14 +373,12 @@ __device__ __forceinline__ void epi_vec8(const GemmParams& p, int row, int col, 
       *reinterpret_cast<floatx4*>(c + 4) = floatx4{v[4], v[5], v[6], v[7]};
     }
     if (p.C16) {
-      u16x8 hi, lo;
+      uint32_t hi[4], lo[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        hi[e] = bf16_rne(v[e]);
-        lo[e] = bf16_rne(v[e] - bf16_to_f32(hi[e]));
-      }
-      *reinterpret_cast<u16x8*>(static_cast<uint16_t*>(p.C16) + off) = hi;
-      if (p.C16lo) *reinterpret_cast<u16x8*>(static_cast<uint16_t*>(p.C16lo) + off) = lo;
+      for (int e = 0; e < 4; ++e) split2_bf16(v[2 * e], v[2 * e + 1], hi[e], lo[e]);
+      *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.C16) + off) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+      if (p.C16lo)
+        *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.C16lo) + off) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
     }
   }
 }
@@ -518,11 +528,16 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_ring_kernel(GemmPara
   constexpr int BM = 16 * TM * WGM;
   constexpr int BN = 16 * TN * WGN;
   constexpr int NW = WGM * WGN;
+  // PASSES 13: bf16x3 as one bf16 GEMM over concatenated operands, K' = 3K:
+  // A' = [A_hi | A_hi | A_lo], W' = [W_hi | W_lo | W_hi] (one LDS plane, one MFMA per step).
+  // Measured slower than the two-plane form on every encoder shape except K = 96 (it
+  // moves 1.5x the operand bytes through the CU's L2 path), so no launcher selects it.
+  constexpr bool KC = PASSES == 13;
   constexpr int PL = PASSES == 3 ? 2 : 1;
   constexpr int ROWB = BK16 * 2;                 // 64 B per tile row
   constexpr int A_BYTES = BM * ROWB, W_BYTES = BN * ROWB;
   constexpr int STAGE = PL * (A_BYTES + W_BYTES);
-  static_assert(NSTAGE == 2 || NSTAGE == 3, "ring depth");
+  static_assert(NSTAGE >= 2 && NSTAGE <= 4, "ring depth");
   // 1-KB DMA pieces (16 rows) per wave per plane; when the pieces do not split evenly
   // (BN = 96: 6 over 4 waves) the spare slots re-load the last piece, identical bytes to
   // the same LDS place, so every wave issues the same count and one vmcnt fits all
@@ -548,7 +563,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_ring_kernel(GemmPara
   tile_of(p.N / BN, tx, ty);
   const int row0 = ty * BM;
   const int col0 = tx * BN;
-  const int nk = p.K / BK16;
+  const int nk = (KC ? 3 : 1) * p.K / BK16;
 
   // per-lane DMA source: piece row = 16*piece + lane/4, chunk lane%4 (swizzled)
   const int prow = lane >> 2;
@@ -572,10 +587,18 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_ring_kernel(GemmPara
   }
   auto issue = [&](int kt) {
     char* st = lds + (kt % NSTAGE) * STAGE;
-    const int kb = kt * ROWB;
+    int kel = kt * BK16;  // k within the (segment's) operand
+    int seg = 0;
+    if constexpr (KC) {
+      seg = kel / p.K;
+      kel -= seg * p.K;
+    }
+    const int kb = kel * 2;
+    const char* Aseg = KC ? Ag[seg == 2 ? 1 : 0] : nullptr;
+    const char* Wseg = KC ? Wg[seg == 1 ? 1 : 0] : nullptr;
     int ky = 0, kx = 0, c0 = 0;
     if constexpr (CONV) {
-      const int k0 = kt * BK16;
+      const int k0 = kel;
       const int tap = k0 / p.conv.Cin;
       c0 = k0 - tap * p.conv.Cin;
       ky = tap / p.conv.ks;
@@ -592,11 +615,12 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_ring_kernel(GemmPara
           const ConvGeom& g = p.conv;
           const int iy = cv_iy[i] + ky, ix = cv_ix[i] + kx;
           const bool ok = cv_b[i] >= 0 && iy >= 0 && iy < g.Hin && ix >= 0 && ix < g.Win;
-          src = ok ? Ag[q] + ((((size_t)cv_b[i] * g.Hin + iy) * g.Win + ix) * g.Cin + c0) * 2 + 16 * (pch ^ swz(r))
+          src = ok ? (KC ? Aseg : Ag[q]) + ((((size_t)cv_b[i] * g.Hin + iy) * g.Win + ix) * g.Cin + c0) * 2 +
+                         16 * (pch ^ swz(r))
                    : static_cast<const char*>(p.zero) + 16 * pch;
         } else {
           const int gr = min(row0 + r, p.M - 1);
-          src = Ag[q] + (size_t)gr * p.lda * 2 + kb + 16 * (pch ^ swz(r));
+          src = (KC ? Aseg : Ag[q]) + (size_t)gr * p.lda * 2 + kb + 16 * (pch ^ swz(r));
         }
         __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(st + q * A_BYTES + pc * 1024), 16, 0, 0);
       }
@@ -604,7 +628,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_ring_kernel(GemmPara
       for (int i = 0; i < W_DMA; ++i) {
         const int pc = min(wave * W_DMA + i, BN / 16 - 1);
         const int r = pc * 16 + prow;
-        const char* src = Wg[q] + (size_t)(col0 + r) * p.ldw * 2 + kb + 16 * (pch ^ swz(r));
+        const char* src = (KC ? Wseg : Wg[q]) + (size_t)(col0 + r) * p.ldw * 2 + kb + 16 * (pch ^ swz(r));
         __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(st + PL * A_BYTES + q * W_BYTES + pc * 1024), 16, 0, 0);
       }
     }
@@ -616,13 +640,16 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_ring_kernel(GemmPara
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  issue(0);
-  if (NSTAGE == 3 && nk > 1) issue(1);
+  for (int k = 0; k < NSTAGE - 1 && k < nk; ++k) issue(k);
   const int l16 = lane & 15;
   const int kq = lane >> 4;  // 16-B chunk of the fragment (k = 8*kq .. 8*kq+7)
   for (int kt = 0; kt < nk; ++kt) {
     // retire tile kt's DMA (tile kt+1's may stay in flight), then make it visible to all waves
-    if (NSTAGE == 3 && kt + 1 < nk) {
+    // tiles kt+1 .. kt+NSTAGE-2 may stay in flight
+    const int ahead = min(NSTAGE - 2, nk - 1 - kt);
+    if (NSTAGE >= 4 && ahead >= 2) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DMA_PER_TILE) : "memory");
+    } else if (NSTAGE >= 3 && ahead >= 1) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_PER_TILE) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -730,6 +757,213 @@ void launch_conv_passes(const GemmParams& p, hipStream_t s) {
     throw std::runtime_error("conv: Cout must be a multiple of 64");
 }
 
+// ---------------------------------------------------------------- 256 x 256 staggered kernel
+// 8 waves (wr = wave / 4: rows 128*wr.., wc = wave % 4: cols 64*wc..), each owning a
+// 128 x 64 output = 4 quadrants of 64 x 32 (4 x 2 MFMA tiles).  A K-tile is 64 k (bf16)
+// or 32 k in hi|lo planes (bf16x3): either way 128-B LDS rows, 32 KB of A + 32 KB of W,
+// two buffers (128 KB).  Each K-tile runs 4 phases (one per quadrant), each phase a LOAD
+// section (the quadrant's fragments by ds_read_b128, the next K-tile's DMA in phases
+// 0-1, lgkmcnt(0)) and a COMPUTE section (the quadrant's MFMAs), separated by raw
+// s_barriers.  Wave group 1 (wr = 1) starts one barrier late, so on every SIMD (one wave
+// of each group) one wave's MFMAs run while the other loads.  Each group drains its
+// DMA (vmcnt(0)) right before the barrier after which the other group first reads the
+// buffer; every LOAD ends with lgkmcnt(0), so a buffer is refilled only after every
+// wave's reads of it completed (the barrier that ends K-tile t-1's last LOAD).
+// LDS row r holds global 16-B chunk c at chunk c ^ ((r >> 1) & 7): the 16 lanes of a
+// ds_read_b128 group (16 consecutive rows, one chunk) hit 16 distinct slots.
+__device__ __forceinline__ int swz8(int r) { return (r >> 1) & 7; }
+
+template <int EPI, int PASSES>
+__global__ void __launch_bounds__(512) gemm_bf16_stag_kernel(GemmParams p) {
+  constexpr int BM = 256, BN = 256;
+  constexpr bool X3 = PASSES == 3;
+  constexpr int KT = X3 ? 32 : 64;        // k per K-tile
+  constexpr int ROWB = 128;               // LDS row bytes
+  constexpr int OPB = 256 * ROWB;         // one operand per buffer: 32 KB
+  constexpr int BUF = 2 * OPB;            // A + W: 64 KB
+  constexpr int EW = 64, ES = EW + 4, ER = 32;
+  static_assert(8 * ER * ES * 4 <= 2 * BUF, "epilogue slab");
+  __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave >> 2;
+  const int wc = wave & 3;
+  int tx, ty;
+  tile_of(p.N / BN, tx, ty);
+  const int row0 = ty * BM;
+  const int col0 = tx * BN;
+  const int nk = p.K / KT;
+  const char* A0 = static_cast<const char*>(p.A);
+  const char* A1 = static_cast<const char*>(X3 ? p.A_lo : p.A);
+  const char* W0 = static_cast<const char*>(p.W);
+  const char* W1 = static_cast<const char*>(X3 ? p.W_lo : p.W);
+
+  // DMA: one glds instruction = 8 rows x 128 B; half-tile h (0,1: A rows 128h..; 2,3: W
+  // rows 128(h-2)..) = 16 instructions, 2 per wave.  Lane: row +lane/8, chunk lane%8.
+  const int drow = lane >> 3;
+  const int dch = lane & 7;
+  auto issue_half = [&](int kt, int h) {
+    char* buf = lds + (kt & 1) * BUF + (h >> 1) * OPB;
+    const int k0 = kt * KT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = (h & 1) * 128 + (wave * 2 + i) * 8 + drow;  // row within the operand tile
+      const int sc = dch ^ swz8(r);                              // global chunk this lane fetches
+      const char* src;
+      if (h < 2) {
+        const size_t gr = (size_t)min(row0 + r, p.M - 1);
+        if constexpr (X3) src = (sc < 4 ? A0 : A1) + (gr * p.lda + k0 + 8 * (sc & 3)) * 2;
+        else src = A0 + (gr * p.lda + k0 + 8 * sc) * 2;
+      } else {
+        const size_t gr = (size_t)(col0 + r);
+        if constexpr (X3) src = (sc < 4 ? W0 : W1) + (gr * p.ldw + k0 + 8 * (sc & 3)) * 2;
+        else src = W0 + (gr * p.ldw + k0 + 8 * sc) * 2;
+      }
+      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(buf + ((h & 1) * 128 + (wave * 2 + i) * 8) * ROWB), 16, 0,
+                                       0);
+    }
+  };
+
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int l16 = lane & 15;
+  const int kq = lane >> 4;
+  // fragments of the current quadrant: A 4 row-tiles x 2 (k-steps or planes), W 2 x 2
+  bf16x8 fa[4][2], fb[2][2];
+  auto load_a = [&](const char* buf, int qm) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = wr * 128 + qm * 64 + i * 16 + l16;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        fa[i][s2] = *reinterpret_cast<const bf16x8*>(buf + r * ROWB + 16 * ((4 * s2 + kq) ^ swz8(r)));
+    }
+  };
+  auto load_b = [&](const char* buf, int qn) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = wc * 64 + qn * 32 + j * 16 + l16;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        fb[j][s2] = *reinterpret_cast<const bf16x8*>(buf + OPB + r * ROWB + 16 * ((4 * s2 + kq) ^ swz8(r)));
+    }
+  };
+  auto compute = [&](int qm, int qn) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        floatx4& c = acc[qm * 4 + i][qn * 2 + j];
+        if constexpr (X3) {  // planes: s2 = 0 hi, 1 lo
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
+        } else {  // k-steps
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
+        }
+      }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: K-tile 0 into buffer 0, visible to all; group 1 then falls one barrier behind
+#pragma unroll
+  for (int h = 0; h < 4; ++h) issue_half(0, h);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();
+
+  // quadrant order (0,0) (0,1) (1,1) (1,0): A changes once, W every other phase
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* buf = lds + (kt & 1) * BUF;
+    const bool more = kt + 1 < nk;
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int qm = (ph == 1 || ph == 2) ? (ph == 2 ? 1 : 0) : (ph == 3 ? 1 : 0);
+      const int qn = (ph == 1 || ph == 2) ? 1 : 0;
+      // LOAD
+      if (ph == 0) {
+        load_b(buf, 0);
+        load_a(buf, 0);
+      } else if (ph == 1) {
+        load_b(buf, 1);
+      } else if (ph == 2) {
+        load_a(buf, 1);
+      } else {
+        load_b(buf, 0);
+      }
+      if (more && ph < 2) {
+        issue_half(kt + 1, 2 * ph);
+        issue_half(kt + 1, 2 * ph + 1);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (ph == 3 && wr == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      // COMPUTE
+      compute(qm, qn);
+      if (ph == 3 && wr == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // pair group 1's extra barrier
+  __builtin_amdgcn_s_barrier();
+
+  // epilogue: per-wave LDS transpose, 32 rows x 64 columns per round
+  float* ep = reinterpret_cast<float*>(lds) + wave * ER * ES;
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ep[(i2 * 16 + 4 * kq + r) * ES + j * 16 + l16] = acc[2 * h + i2][j][r];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int it = 0; it < ER * EW / 8 / 64; ++it) {
+      const int idx = it * 64 + lane;
+      const int rr = idx / (EW / 8);
+      const int cc = idx - rr * (EW / 8);
+      const floatx4 v0 = *reinterpret_cast<const floatx4*>(ep + rr * ES + cc * 8);
+      const floatx4 v1 = *reinterpret_cast<const floatx4*>(ep + rr * ES + cc * 8 + 4);
+      float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      const int row = row0 + wr * 128 + h * 32 + rr;
+      if (row < p.M) epi_vec8<EPI>(p, row, col0 + wc * EW + cc * 8, v);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// Staggered 256 x 256 kernel: measured (B=64, 384²) faster than the ring kernels on bf16x3
+// GEMMs with K <= N and enough tiles (s3.fc1 225 -> 217 us, s4.fc1 163 -> 154), slower with
+// K > N or few tiles and in plain bf16.  MOCR_GEMM_STAG_MIN: minimum tiles (default 384;
+// set it to 1 to force the kernel wherever N % 256 == 0, as the bitwise A/B does).
+template <int PASSES>
+bool try_stag(const GemmParams& p, hipStream_t s) {
+  static const char* env = getenv("MOCR_GEMM_STAG_MIN");
+  static const long min_tiles = env ? atol(env) : 384;
+  if (min_tiles <= 0 || p.N % 256 != 0 || p.K % (PASSES == 3 ? 32 : 64) != 0) return false;
+  if (!env && (PASSES != 3 || p.K > p.N)) return false;
+  const long tiles = (long)((p.M + 255) / 256) * (p.N / 256);
+  if (tiles < min_tiles) return false;
+  const dim3 grid((unsigned)tiles);
+  switch (p.epi) {
+    case EPI_STORE: gemm_bf16_stag_kernel<EPI_STORE, PASSES><<<grid, 512, 0, s>>>(p); break;
+    case EPI_GELU: gemm_bf16_stag_kernel<EPI_GELU, PASSES><<<grid, 512, 0, s>>>(p); break;
+    case EPI_RESADD: gemm_bf16_stag_kernel<EPI_RESADD, PASSES><<<grid, 512, 0, s>>>(p); break;
+    case EPI_WINRES: gemm_bf16_stag_kernel<EPI_WINRES, PASSES><<<grid, 512, 0, s>>>(p); break;
+    default: throw std::runtime_error("gemm_bf16: bad epilogue");
+  }
+  return true;
+}
+
 // 256-row tiles: 8 waves as 2 (M) x 4 (N), each 128 x 16*TN, 2-stage ring (bf16x3: 2 x
 // 64 KB of LDS, 1 block per CU).  Half the operand re-reads per MFMA of the 128-row
 // tiles, but one k-tile in flight at one block per CU: measured (B=64, 384²) faster on
@@ -767,10 +1001,25 @@ bool try_big_tile(const GemmParams& p, hipStream_t s) {
   return true;
 }
 
+template <int TM, int TN, int WGM, int WGN, int PASSES, int NST>
+void launch_ring(const GemmParams& p, hipStream_t s) {
+  constexpr int BM = 16 * TM * WGM, BN = 16 * TN * WGN;
+  const dim3 grid((p.N / BN) * ((p.M + BM - 1) / BM));
+  const dim3 block(64 * WGM * WGN);
+  switch (p.epi) {
+    case EPI_STORE: gemm_bf16_ring_kernel<TM, TN, WGM, WGN, EPI_STORE, PASSES, NST><<<grid, block, 0, s>>>(p); break;
+    case EPI_GELU: gemm_bf16_ring_kernel<TM, TN, WGM, WGN, EPI_GELU, PASSES, NST><<<grid, block, 0, s>>>(p); break;
+    case EPI_RESADD: gemm_bf16_ring_kernel<TM, TN, WGM, WGN, EPI_RESADD, PASSES, NST><<<grid, block, 0, s>>>(p); break;
+    case EPI_WINRES: gemm_bf16_ring_kernel<TM, TN, WGM, WGN, EPI_WINRES, PASSES, NST><<<grid, block, 0, s>>>(p); break;
+    default: throw std::runtime_error("gemm_bf16: bad epilogue");
+  }
+}
+
 template <int PASSES>
 void launch_bf16_passes(const GemmParams& p, hipStream_t s) {
   // MOCR_GEMM_RING = 0 (register staging) | 2 | 3 (LDS-DMA ring depth); A/B switch
   static const int ring = getenv("MOCR_GEMM_RING") ? atoi(getenv("MOCR_GEMM_RING")) : 2;
+  if (ring == 2 && try_stag<PASSES>(p, s)) return;
   if (ring == 2 && try_big_tile<PASSES>(p, s)) return;
   if (p.N % 128 == 0) {  // 128 x 128, waves of 64 x 64
     if (ring == 3)

@@ -138,16 +138,11 @@ __global__ void __launch_bounds__(256) ln_group_kernel(const float* __restrict__
   for (int e = 0; e < F; e += 4) {
     if (out.f32) *reinterpret_cast<floatx4*>(out.f32 + off + e) = floatx4{v[e], v[e + 1], v[e + 2], v[e + 3]};
     if (out.hi) {
-      uint16_t h[4], l[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        h[k] = f32_to_bf16_rne(v[e + k]);
-        l[k] = f32_to_bf16_rne(v[e + k] - __uint_as_float((uint32_t)h[k] << 16));
-      }
-      *reinterpret_cast<uint2*>(out.hi + off + e) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
-      if (out.lo)
-        *reinterpret_cast<uint2*>(out.lo + off + e) =
-            make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+      uint32_t h0, l0, h1, l1;
+      split2_bf16(v[e], v[e + 1], h0, l0);
+      split2_bf16(v[e + 2], v[e + 3], h1, l1);
+      *reinterpret_cast<uint2*>(out.hi + off + e) = make_uint2(h0, h1);
+      if (out.lo) *reinterpret_cast<uint2*>(out.lo + off + e) = make_uint2(l0, l1);
     }
   }
 }
@@ -399,12 +394,11 @@ typedef __bf16 abf16x8 __attribute__((ext_vector_type(8)));
 typedef uint16_t au16x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ void split8(const float (&x)[8], abf16x8& hi, abf16x8& lo) {
-  au16x8 h, l;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    h[e] = f32_to_bf16_rne(x[e]);
-    l[e] = f32_to_bf16_rne(x[e] - __uint_as_float((uint32_t)h[e] << 16));
-  }
+  uint4 h, l;
+  split2_bf16(x[0], x[1], h.x, l.x);
+  split2_bf16(x[2], x[3], h.y, l.y);
+  split2_bf16(x[4], x[5], h.z, l.z);
+  split2_bf16(x[6], x[7], h.w, l.w);
   hi = __builtin_bit_cast(abf16x8, h);
   lo = __builtin_bit_cast(abf16x8, l);
 }
@@ -540,17 +534,11 @@ __global__ void __launch_bounds__(256) window_attention_mfma_kernel(const float*
         const size_t off = ((size_t)win_g * kWinTok + q) * C + h * kHeadDim + 16 * dt + 4 * g;
         if (out.f32) *reinterpret_cast<floatx4*>(out.f32 + off) = o;
         if (out.hi) {
-          uint16_t hs[4], ls[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            hs[r] = f32_to_bf16_rne(o[r]);
-            ls[r] = f32_to_bf16_rne(o[r] - __uint_as_float((uint32_t)hs[r] << 16));
-          }
-          *reinterpret_cast<uint2*>(out.hi + off) =
-              make_uint2(hs[0] | ((uint32_t)hs[1] << 16), hs[2] | ((uint32_t)hs[3] << 16));
-          if (out.lo)
-            *reinterpret_cast<uint2*>(out.lo + off) =
-                make_uint2(ls[0] | ((uint32_t)ls[1] << 16), ls[2] | ((uint32_t)ls[3] << 16));
+          uint32_t h0, l0, h1, l1;
+          split2_bf16(o[0], o[1], h0, l0);
+          split2_bf16(o[2], o[3], h1, l1);
+          *reinterpret_cast<uint2*>(out.hi + off) = make_uint2(h0, h1);
+          if (out.lo) *reinterpret_cast<uint2*>(out.lo + off) = make_uint2(l0, l1);
         }
       }
     }
