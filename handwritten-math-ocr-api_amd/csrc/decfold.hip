@@ -1,0 +1,421 @@
+// Folded greedy decode step (kernels.h FoldGemmParams / FoldAttnParams): 5 dependent
+// kernels per nn.TransformerDecoderLayer (torch/nn/modules/transformer.py:1143-1199)
+// instead of 8.
+//
+// In a post-norm layer every projection reads a LayerNorm of a pre-norm sum y, which
+// needs y's whole row.  For LN(y) = g (y - mu) rstd + b feeding W x + c:
+//   W LN(y) + c = rstd (W' y - mu s) + c',   W' = W diag(g), s = W g, c' = W b + c,
+// and W' y expands over y's own terms (y = residual + W_o a + b_o), so z = W' y is one
+// more column block of the kernel that produces y, and the consumer only applies rstd,
+// mu (y's slice statistics, merged as every other consumer merges them), s and c'.
+// The CA q projection moves into the SA out-projection, FFN1 into the CA out-projection,
+// the next layer's q|k|v projection into FFN2 (whose hidden is unfolded on load), and
+// layer 0's q|k|v of a fed token into a [V, 3d] + [max_pos, 3d] table lookup.  The fold
+// changes fp32 rounding only (weights folded with fp64 accumulation at load time).
+//
+// Loads are never predicated per element: out-of-range rows / keys read a clamped valid
+// address and are masked after the load (hipcc turns `c ? *p : 0` into a branch and a
+// full vmcnt(0) wait per element).
+#include "kernels.h"
+
+namespace mocr {
+
+namespace {
+
+constexpr int kD = 256;
+constexpr int kSlices = kD / 16;
+constexpr float kAttnScale = 0.17677669529663687f;  // 1/sqrt(32)
+
+__device__ __forceinline__ float ln_apply(float v, float mean, float rstd, float g, float b) {
+  return fmaf((v - mean) * rstd, g, b);
+}
+
+// Row statistics from 16 (mean, M2) slice partials, merged by the fixed binary tree of
+// decoder.hip (Chan et al.), so the values are bit-identical to every other consumer's.
+__device__ __forceinline__ void merge_eq(float& m, float& q, float mb, float qb, float n) {
+  const float delta = mb - m;
+  q = q + qb + delta * delta * (n * 0.5f);
+  m = m + delta * 0.5f;
+}
+__device__ __forceinline__ void merge_lanes(float& m, float& q, int mask, bool upper, float n) {
+  const float mo = __shfl_xor(m, mask, 64);
+  const float qo = __shfl_xor(q, mask, 64);
+  if (upper) {
+    float mm = mo, qq = qo;
+    merge_eq(mm, qq, m, q, n);
+    m = mm;
+    q = qq;
+  } else {
+    merge_eq(m, q, mo, qo, n);
+  }
+}
+__device__ __forceinline__ float rstd_of(float m2) { return 1.0f / sqrtf(m2 * (1.0f / kD) + 1e-5f); }
+// Layout 1 of decoder.hip: lane group g = 0..3 of a row holds slices 4g..4g+3 (loaded
+// first, merged later, so several rows' partials can be in flight together).
+struct Part4 {
+  floatx4 p0, p1;
+};
+__device__ __forceinline__ Part4 load_part4(const float* __restrict__ part, int g) {
+  return {*reinterpret_cast<const floatx4*>(part + 8 * g), *reinterpret_cast<const floatx4*>(part + 8 * g + 4)};
+}
+__device__ __forceinline__ void merge_part4(const Part4& pp, int g, float& mean, float& rstd) {
+  const floatx4 p0 = pp.p0, p1 = pp.p1;
+  float m = p0[0], q = p0[1], m2 = p1[0], q2 = p1[1];
+  merge_eq(m, q, p0[2], p0[3], 16.f);
+  merge_eq(m2, q2, p1[2], p1[3], 16.f);
+  merge_eq(m, q, m2, q2, 32.f);
+  merge_lanes(m, q, 16, (g & 1) != 0, 64.f);
+  merge_lanes(m, q, 32, (g & 2) != 0, 128.f);
+  mean = m;
+  rstd = rstd_of(q);
+}
+__device__ __forceinline__ void row_stats_16lanes(const float* __restrict__ part, int c, float& mean, float& rstd) {
+  float m = part[2 * c], q = part[2 * c + 1];
+  merge_lanes(m, q, 1, (c & 1) != 0, 16.f);
+  merge_lanes(m, q, 2, (c & 2) != 0, 32.f);
+  merge_lanes(m, q, 4, (c & 4) != 0, 64.f);
+  merge_lanes(m, q, 8, (c & 8) != 0, 128.f);
+  mean = m;
+  rstd = rstd_of(q);
+}
+
+// ------------------------------------------------------------------ fold row GEMM
+// Workgroups x < 16 own a 16x16 tile of y (K = K1 over A1'), the others a 16x16 tile of
+// z (K = K1 + d over [A1' | A2']).  4 waves split K and combine through LDS in a fixed
+// order on v_mfma_f32_16x16x4_f32, as decoder.hip rowgemm_kernel; the y epilogue is its
+// DEC_RESADD (y = A2' + (acc + by), then the (mean, M2) of the tile's 16 columns).  The
+// 16-wide k chunks never straddle A1 / A2 (K1 % 16 == 0), so a chunk's source is
+// wave-uniform.  S1 / S2: A1 / A2 carry statistics (unfold / LayerNorm on load).
+template <int NI, bool YT, bool S1, bool S2>
+__device__ __forceinline__ void fold_tile(const FoldGemmParams& p, int c0) {
+  __shared__ float red[4][16][17];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int r0 = blockIdx.y * 16;
+  const int ra = min(r0 + (lane & 15), p.B - 1);  // rows >= B compute discarded outputs
+  const int cb = c0 + (lane & 15);
+  const int g = lane >> 4;
+  const int kbeg = wave * NI * 16;
+  const int K1 = p.K1;
+  const float* wrow = YT ? p.Wy + (size_t)cb * K1 : p.Wz + (size_t)cb * (K1 + kD);
+
+  // every independent load first: A, W, the unfold / LayerNorm vectors, the residual
+  floatx4 a[NI], b[NI], u[NI], v[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int k = kbeg + i * 16 + 4 * g;
+    const bool in1 = k < K1;
+    b[i] = *reinterpret_cast<const floatx4*>(wrow + k);
+    a[i] = *reinterpret_cast<const floatx4*>(in1 ? p.A1 + (size_t)ra * K1 + k : p.A2 + (size_t)ra * kD + (k - K1));
+    if constexpr (S1 || S2) {
+      const float* us = in1 ? (S1 ? p.a1_s + k : p.a2_g) : (S2 ? p.a2_g + (k - K1) : p.a1_s);
+      const float* vs = in1 ? (S1 ? p.a1_c + k : p.a2_b) : (S2 ? p.a2_b + (k - K1) : p.a1_c);
+      u[i] = *reinterpret_cast<const floatx4*>(us);
+      v[i] = *reinterpret_cast<const floatx4*>(vs);
+    }
+  }
+  const int row = tid >> 4;
+  const int col = tid & 15;
+  const int grow = r0 + row;
+  const int gcol = c0 + col;
+  const int rrow = min(grow, p.B - 1);
+  float rres = 0.f, rg = 0.f, rb = 0.f;
+  if constexpr (YT) {
+    rres = p.A2[(size_t)rrow * kD + gcol];
+    if constexpr (S2) {
+      rg = p.a2_g[gcol];
+      rb = p.a2_b[gcol];
+    }
+  }
+  const size_t srow = (size_t)ra * 2 * kSlices;
+  Part4 pa1{}, pa2{};
+  if constexpr (S1) pa1 = load_part4(p.a1_stats + srow, g);
+  if constexpr (S2) pa2 = load_part4(p.a2_stats + srow, g);
+  float m1 = 0.f, r1 = 0.f, m2 = 0.f, r2 = 0.f;
+  if constexpr (S1) merge_part4(pa1, g, m1, r1);
+  if constexpr (S2) merge_part4(pa2, g, m2, r2);
+  if constexpr (S1 || S2) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int k = kbeg + i * 16 + 4 * g;
+      if (k < K1) {
+        if constexpr (S1)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) a[i][s] = fmaxf(fmaf(r1, fmaf(-m1, u[i][s], a[i][s]), v[i][s]), 0.f);
+      } else {
+        if constexpr (S2)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) a[i][s] = ln_apply(a[i][s], m2, r2, u[i][s], v[i][s]);
+      }
+    }
+  }
+
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[i][s], acc, 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wave][g * 4 + r][lane & 15] = acc[r];
+  __syncthreads();
+  if constexpr (YT && S2) {  // all 16 lanes of a row take part in the merge
+    float mean, rstd;
+    row_stats_16lanes(p.a2_stats + (size_t)rrow * 2 * kSlices, col, mean, rstd);
+    rres = ln_apply(rres, mean, rstd, rg, rb);
+  }
+  if (grow >= p.B || dec_skip(p.st, p.t)) return;  // uniform per 16-lane row group
+  const float val = ((red[0][row][col] + red[1][row][col]) + red[2][row][col]) + red[3][row][col];
+  if constexpr (YT) {
+    const float y = rres + (val + p.by[gcol]);
+    p.y[(size_t)grow * kD + gcol] = y;
+    float s = y;
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    s += __shfl_xor(s, 8, 64);
+    const float m16 = s * (1.0f / 16);
+    float q = (y - m16) * (y - m16);
+    q += __shfl_xor(q, 1, 64);
+    q += __shfl_xor(q, 2, 64);
+    q += __shfl_xor(q, 4, 64);
+    q += __shfl_xor(q, 8, 64);
+    if (col == 0) {
+      float* so = p.y_stats + ((size_t)grow * kSlices + c0 / 16) * 2;
+      so[0] = m16;
+      so[1] = q;
+    }
+  } else {
+    p.z[(size_t)grow * p.NZ + gcol] = val + p.bz[gcol];
+  }
+}
+
+template <int K1, bool S1, bool S2>
+__global__ void __launch_bounds__(256) foldgemm_kernel(FoldGemmParams p) {
+  if (blockIdx.x < kD / 16)
+    fold_tile<K1 / 64, true, S1, S2>(p, blockIdx.x * 16);
+  else
+    fold_tile<(K1 + kD) / 64, false, S1, S2>(p, (blockIdx.x - kD / 16) * 16);
+}
+
+// ------------------------------------------------------------------ fold attention
+// The newest position of row b against n keys for head h (one workgroup, 4 waves): the
+// key loop of decoder.hip dec_attn_kernel (8 lanes per 32-float key row slice, every
+// K/V load issued up front, per-wave softmax, wave partials merged after one barrier).
+// Each lane unfolds its 4 columns of q -- and, self-attention, of the new k and v --
+// from z; the lanes of key slot t take the new k/v from registers, and wave 0's first
+// key group appends them to the cache.  ZS: z carries statistics (else z is final).
+template <bool SELF, bool ZS, int NIT>
+__global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
+  constexpr int LPR = 8;  // lanes per key row
+  constexpr int RPW = 8;  // key rows per wave instruction
+  __shared__ floatx4 po[4][LPR];
+  __shared__ float pm[4], ps[4];
+
+  const int b = blockIdx.x;
+  const int h = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int rsub = lane / LPR;
+  const int li = lane % LPR;
+  const int cc = h * 32 + li * 4;  // this lane's 4 columns of the head
+  const int t = p.t;
+  const int n = p.n;
+  const int n_cached = SELF ? t : n;
+  const int m_first = wave * RPW + rsub;
+
+  const float* Kb = p.K + (size_t)b * p.kv_b_stride + cc;
+  const float* Vb = p.V + (size_t)b * p.kv_b_stride + cc;
+  floatx4 kk[NIT], vv[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int m = m_first + it * 4 * RPW;
+    const size_t ml = (size_t)(m < n_cached ? m : 0);  // row 0 is allocated; masked below
+    kk[it] = *reinterpret_cast<const floatx4*>(Kb + ml * p.kv_row_stride);
+    vv[it] = *reinterpret_cast<const floatx4*>(Vb + ml * p.kv_row_stride);
+  }
+  constexpr int NP = SELF ? 3 : 1;  // q (| k | v)
+  const float* zr = p.z + (size_t)b * p.z_ld + cc;
+  floatx4 zv[NP], sv[NP], cv[NP];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    zv[j] = *reinterpret_cast<const floatx4*>(zr + j * kD);
+    if constexpr (ZS) {
+      sv[j] = *reinterpret_cast<const floatx4*>(p.s + j * kD + cc);
+      cv[j] = *reinterpret_cast<const floatx4*>(p.c + j * kD + cc);
+    }
+  }
+  if constexpr (ZS) {
+    float mean, rstd;
+    row_stats_16lanes(p.z_stats + (size_t)b * 2 * kSlices, lane & 15, mean, rstd);
+#pragma unroll
+    for (int j = 0; j < NP; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) zv[j][e] = fmaf(rstd, fmaf(-mean, sv[j][e], zv[j][e]), cv[j][e]);
+  }
+  const floatx4 q4 = zv[0];
+  const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int m = m_first + it * 4 * RPW;
+    if constexpr (SELF) {
+      kk[it] = m == t ? zv[1] : kk[it];
+      vv[it] = m == t ? zv[2] : (m < t ? vv[it] : zero);
+    } else {
+      vv[it] = m < n ? vv[it] : zero;
+    }
+  }
+  if constexpr (SELF) {
+    if (wave == 0 && rsub == 0 && !dec_skip(p.st, t)) {
+      const size_t o = (size_t)b * p.kv_b_stride + (size_t)t * p.kv_row_stride + cc;
+      *reinterpret_cast<floatx4*>(p.kcache + o) = zv[1];
+      *reinterpret_cast<floatx4*>(p.vcache + o) = zv[2];
+    }
+  }
+
+  float sc[NIT];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    float s = q4[0] * kk[it][0];
+    s = fmaf(q4[1], kk[it][1], s);
+    s = fmaf(q4[2], kk[it][2], s);
+    s = fmaf(q4[3], kk[it][3], s);
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    s *= kAttnScale;
+    sc[it] = (m_first + it * 4 * RPW < n) ? s : -INFINITY;
+    mx = fmaxf(mx, sc[it]);
+  }
+#pragma unroll
+  for (int o = LPR; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  float sum = 0.f;
+  floatx4 o4 = {0.f, 0.f, 0.f, 0.f};
+  if (mx != -INFINITY) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const float e = expf(sc[it] - mx);
+      sum += e;
+      o4[0] = fmaf(e, vv[it][0], o4[0]);
+      o4[1] = fmaf(e, vv[it][1], o4[1]);
+      o4[2] = fmaf(e, vv[it][2], o4[2]);
+      o4[3] = fmaf(e, vv[it][3], o4[3]);
+    }
+  }
+#pragma unroll
+  for (int o = LPR; o < 64; o <<= 1) {
+    sum += __shfl_xor(sum, o, 64);
+    o4[0] += __shfl_xor(o4[0], o, 64);
+    o4[1] += __shfl_xor(o4[1], o, 64);
+    o4[2] += __shfl_xor(o4[2], o, 64);
+    o4[3] += __shfl_xor(o4[3], o, 64);
+  }
+  if (rsub == 0) {
+    po[wave][li] = o4;
+    if (li == 0) {
+      pm[wave] = mx;
+      ps[wave] = sum;
+    }
+  }
+  __syncthreads();
+  if (tid < 32 && !dec_skip(p.st, t)) {
+    float m = pm[0];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) m = fmaxf(m, pm[w]);
+    float num = 0.f, den = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float f = pm[w] == -INFINITY ? 0.f : expf(pm[w] - m);
+      num = fmaf(po[w][tid / 4][tid % 4], f, num);
+      den = fmaf(ps[w], f, den);
+    }
+    p.out[(size_t)b * kD + h * 32 + tid] = num / den;
+  }
+}
+
+// ------------------------------------------------------------------ load-time folding
+// out[i, j] = sum_k A[i, k] g[k] Bm[k sbk + j sbj] (+ add_row[i] + add_col[j]) in fp64,
+// rounded once to fp32; Bm null: out = A diag(g).
+__global__ void __launch_bounds__(256) fold_mm_kernel(const float* __restrict__ A, int lda,
+                                                      const float* __restrict__ g, const float* __restrict__ Bm,
+                                                      long sbk, long sbj, int K, const float* __restrict__ add_row,
+                                                      const float* __restrict__ add_col, float* __restrict__ out,
+                                                      int ldo, int cols) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = blockIdx.y;
+  if (j >= cols) return;
+  const float* a = A + (size_t)i * lda;
+  double acc = 0.0;
+  if (Bm) {
+    for (int k = 0; k < K; ++k)
+      acc += (double)a[k] * (g ? (double)g[k] : 1.0) * (double)Bm[(long)k * sbk + (long)j * sbj];
+  } else {
+    acc = (double)a[j] * (g ? (double)g[j] : 1.0);
+  }
+  if (add_row) acc += (double)add_row[i];
+  if (add_col) acc += (double)add_col[j];
+  out[(size_t)i * ldo + j] = (float)acc;
+}
+
+}  // namespace
+
+void launch_foldgemm(const FoldGemmParams& p, hipStream_t s) {
+  if (p.NZ < 0 || p.NZ % 16 != 0 || (p.NZ && (!p.Wz || !p.bz || !p.z)))
+    throw std::runtime_error("foldgemm: NZ must be a multiple of 16 with Wz, bz, z");
+  const bool s1 = p.a1_stats != nullptr, s2 = p.a2_stats != nullptr;
+  if ((s1 && (!p.a1_s || !p.a1_c)) || (s2 && (!p.a2_g || !p.a2_b)))
+    throw std::runtime_error("foldgemm: statistics need their vectors");
+  if (!p.A1 || !p.A2 || !p.Wy || !p.by || !p.y || !p.y_stats) throw std::runtime_error("foldgemm: null operand");
+  if (p.B <= 0) return;
+  const dim3 grid(kD / 16 + p.NZ / 16, (p.B + 15) / 16);
+  if (p.K1 == 256 && !s1 && !s2)
+    foldgemm_kernel<256, false, false><<<grid, 256, 0, s>>>(p);
+  else if (p.K1 == 256 && !s1 && s2)
+    foldgemm_kernel<256, false, true><<<grid, 256, 0, s>>>(p);
+  else if (p.K1 == 512 && s1 && s2)
+    foldgemm_kernel<512, true, true><<<grid, 256, 0, s>>>(p);
+  else
+    throw std::runtime_error("foldgemm: built for (K1 256, A2 plain or LayerNorm) and (K1 512, both)");
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_dec_foldattn(const FoldAttnParams& p, bool self_attn, hipStream_t s) {
+  if (p.n < 1 || p.n > 288) throw std::runtime_error("foldattn: 1..288 keys");
+  const bool zs = p.z_stats != nullptr;
+  if (zs && (!p.s || !p.c)) throw std::runtime_error("foldattn: statistics need s and c");
+  if (self_attn && (!p.kcache || !p.vcache || p.n != p.t + 1 || p.z_ld < 3 * kD))
+    throw std::runtime_error("foldattn: self-attention needs the cache, n = t + 1 and q|k|v");
+  if (p.B <= 0) return;
+  const int nit = (p.n + 31) / 32;  // 32 key rows per workgroup pass (4 waves x 8 rows)
+  const dim3 grid(p.B, kD / 32);
+#define MOCR_FA(N)                                                                    \
+  case N:                                                                             \
+    if (self_attn && zs)                                                              \
+      dec_foldattn_kernel<true, true, N><<<grid, 256, 0, s>>>(p);                     \
+    else if (self_attn)                                                               \
+      dec_foldattn_kernel<true, false, N><<<grid, 256, 0, s>>>(p);                    \
+    else if (zs)                                                                      \
+      dec_foldattn_kernel<false, true, N><<<grid, 256, 0, s>>>(p);                    \
+    else                                                                              \
+      dec_foldattn_kernel<false, false, N><<<grid, 256, 0, s>>>(p);                   \
+    break;
+  switch (nit) {
+    MOCR_FA(1) MOCR_FA(2) MOCR_FA(3) MOCR_FA(4) MOCR_FA(5) MOCR_FA(6) MOCR_FA(7) MOCR_FA(8) MOCR_FA(9)
+    default: throw std::runtime_error("foldattn: at most 288 keys");
+  }
+#undef MOCR_FA
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_fold_mm(const float* A, int lda, const float* g, const float* Bm, long sbk, long sbj, int K,
+                    const float* add_row, const float* add_col, float* out, int ldo, int rows, int cols,
+                    hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return;
+  const dim3 grid((cols + 255) / 256, rows);
+  fold_mm_kernel<<<grid, 256, 0, s>>>(A, lda, g, Bm, sbk, sbj, K, add_row, add_col, out, ldo, cols);
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace mocr

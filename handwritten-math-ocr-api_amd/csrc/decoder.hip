@@ -108,6 +108,7 @@ __global__ void __launch_bounds__(256) rowgemm_kernel(RowGemmParams p) {
   const int g = lane >> 4;
   const int kbeg = wave * KW;
   const bool row_ok = ra < p.B;
+  const int rc = row_ok ? ra : p.B - 1;  // loads are never predicated (see dec_argmax_kernel)
 
   // issue every independent load first: A, W, LayerNorm affine, residual
   floatx4 a[NI], b[NI];
@@ -115,7 +116,8 @@ __global__ void __launch_bounds__(256) rowgemm_kernel(RowGemmParams p) {
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     const int k = kbeg + i * 16 + 4 * g;
-    a[i] = row_ok ? *reinterpret_cast<const floatx4*>(p.A + (size_t)ra * p.K + k) : floatx4{0.f, 0.f, 0.f, 0.f};
+    a[i] = *reinterpret_cast<const floatx4*>(p.A + (size_t)rc * p.K + k);
+    if (!row_ok) a[i] = floatx4{0.f, 0.f, 0.f, 0.f};
     b[i] = *reinterpret_cast<const floatx4*>(p.W + (size_t)cb * p.K + k);
     if constexpr (ALN) {
       gg[i] = *reinterpret_cast<const floatx4*>(p.a_ln_g + k);
@@ -128,13 +130,11 @@ __global__ void __launch_bounds__(256) rowgemm_kernel(RowGemmParams p) {
   const int gcol = c0 + col;
   const bool out_ok = grow < p.B && gcol < p.n_valid;
   float rres = 0.f, rg = 0.f, rb = 0.f;
-  if constexpr (EPI == DEC_RESADD) {
-    if (out_ok) {
-      rres = p.resid[(size_t)grow * p.ldo + gcol];
-      if constexpr (RLN) {
-        rg = p.r_ln_g[gcol];
-        rb = p.r_ln_b[gcol];
-      }
+  if constexpr (EPI == DEC_RESADD) {  // N == n_valid == d: only the row can be out of range
+    rres = p.resid[(size_t)min(grow, p.B - 1) * p.ldo + gcol];
+    if constexpr (RLN) {
+      rg = p.r_ln_g[gcol];
+      rb = p.r_ln_b[gcol];
     }
   }
   if constexpr (ALN) {
@@ -234,10 +234,13 @@ void launch_rowgemm_e(const RowGemmParams& p, dim3 grid, hipStream_t s) {
 // x[b] = embedding[feed[b][0]] + pos_encoder[0]   (src/model_swin.py:73-75).
 __global__ void __launch_bounds__(256) dec_embed0_kernel(const int32_t* __restrict__ feed, int ld_ids,
                                                          const float* __restrict__ emb, const float* __restrict__ pos,
-                                                         float* __restrict__ x, int d) {
+                                                         float* __restrict__ x, int d, const float* __restrict__ qtab,
+                                                         const float* __restrict__ qpos, float* __restrict__ z) {
   const int b = blockIdx.x;
   const int tok = feed[(size_t)b * ld_ids];
   for (int c = threadIdx.x; c < d; c += blockDim.x) x[(size_t)b * d + c] = emb[(size_t)tok * d + c] + pos[c];
+  if (qtab)
+    for (int c = threadIdx.x; c < 3 * d; c += blockDim.x) z[(size_t)b * 3 * d + c] = qtab[(size_t)tok * 3 * d + c] + qpos[c];
 }
 
 // ------------------------------------------------------------------ attention
@@ -281,16 +284,18 @@ __global__ void __launch_bounds__(256) dec_attn_kernel(const DecodeState* st, in
 
   floatx4 kk[NIT], vv[NIT];
 #pragma unroll
-  for (int it = 0; it < NIT; ++it) {
+  for (int it = 0; it < NIT; ++it) {  // unpredicated loads of a clamped key row, masked after
     const int m = m_first + it * 4 * RPW;
-    if (m < n) {
-      kk[it] = *reinterpret_cast<const floatx4*>(Kb + (size_t)m * kv_row_stride);
-      vv[it] = *reinterpret_cast<const floatx4*>(Vb + (size_t)m * kv_row_stride);
-    } else {
+    const size_t ml = (size_t)(m < n ? m : 0);
+    kk[it] = *reinterpret_cast<const floatx4*>(Kb + ml * kv_row_stride);
+    vv[it] = *reinterpret_cast<const floatx4*>(Vb + ml * kv_row_stride);
+  }
+#pragma unroll
+  for (int it = 0; it < NIT; ++it)
+    if (m_first + it * 4 * RPW >= n) {
       kk[it] = floatx4{0.f, 0.f, 0.f, 0.f};
       vv[it] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
-  }
   float sc[NIT];
   float mx = -INFINITY;
 #pragma unroll
@@ -752,7 +757,8 @@ __global__ void __launch_bounds__(256) dec_argmax_kernel(DecodeState* st, int t,
                                                          float* __restrict__ logp, int32_t* __restrict__ finished,
                                                          int eos, int stop_batch, const float* __restrict__ emb,
                                                          const float* __restrict__ pos, float* __restrict__ x,
-                                                         int d) {
+                                                         int d, const float* __restrict__ qtab,
+                                                         const float* __restrict__ qpos, float* __restrict__ z) {
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -764,8 +770,12 @@ __global__ void __launch_bounds__(256) dec_argmax_kernel(DecodeState* st, int t,
   constexpr int CH = 20;  // loads in flight per thread: one round for V <= 5120
   for (int j0 = tid; j0 < V; j0 += 256 * CH) {
     float vals[CH];
+    // unpredicated loads (a clamped column), masked after: a predicated load per element
+    // becomes a branch + vmcnt(0) each
 #pragma unroll
-    for (int c = 0; c < CH; ++c) vals[c] = (j0 + 256 * c < V) ? L[j0 + 256 * c] : -INFINITY;
+    for (int c = 0; c < CH; ++c) vals[c] = L[min(j0 + 256 * c, V - 1)];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) vals[c] = (j0 + 256 * c < V) ? vals[c] : -INFINITY;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const float v = vals[c];
@@ -829,6 +839,9 @@ __global__ void __launch_bounds__(256) dec_argmax_kernel(DecodeState* st, int t,
   if (!last_step) {
     const int tok = s_next;
     for (int c = tid; c < d; c += 256) x[(size_t)b * d + c] = emb[(size_t)tok * d + c] + pos[(size_t)(t + 1) * d + c];
+    if (qtab)  // folded step: layer 0's q|k|v of the fed token at position t+1
+      for (int c = tid; c < 3 * d; c += 256)
+        z[(size_t)b * 3 * d + c] = qtab[(size_t)tok * 3 * d + c] + qpos[(size_t)(t + 1) * 3 * d + c];
   }
 }
 
@@ -850,8 +863,8 @@ void launch_rowgemm(const RowGemmParams& p, hipStream_t s) {
 }
 
 void launch_dec_embed0(const int32_t* feed, int ld_ids, const float* emb, const float* pos, float* x, int B, int d,
-                       hipStream_t s) {
-  dec_embed0_kernel<<<B, 256, 0, s>>>(feed, ld_ids, emb, pos, x, d);
+                       hipStream_t s, const float* qtab, const float* qpos, float* z) {
+  dec_embed0_kernel<<<B, 256, 0, s>>>(feed, ld_ids, emb, pos, x, d, qtab, qpos, z);
   MOCR_HIP_CHECK(hipGetLastError());
 }
 
@@ -883,9 +896,9 @@ void launch_dec_attn(const DecodeState* st, int t, const float* q, const float* 
 void launch_dec_argmax(DecodeState* st, int t, int last_step, const float* logits, size_t hist_stride, int ldl,
                        int V, int B, int32_t* ids, int32_t* feed, const int32_t* forced, int ld_ids, float* logp,
                        int32_t* finished, int eos, int stop_batch, const float* emb, const float* pos, float* x,
-                       int d, hipStream_t s) {
+                       int d, hipStream_t s, const float* qtab, const float* qpos, float* z) {
   dec_argmax_kernel<<<B, 256, 0, s>>>(st, t, last_step, logits, hist_stride, ldl, V, ids, feed, forced, ld_ids, logp,
-                                      finished, eos, stop_batch, emb, pos, x, d);
+                                      finished, eos, stop_batch, emb, pos, x, d, qtab, qpos, z);
   MOCR_HIP_CHECK(hipGetLastError());
 }
 

@@ -319,6 +319,16 @@ struct mocr_engine {
   int32_t* bseq[2] = {nullptr, nullptr};
   int32_t* bslot[2] = {nullptr, nullptr};
   std::map<std::tuple<int, int, int>, hipGraphExec_t> graphs;
+  // folded greedy step (kernels.h FoldGemmParams): per-layer folded weights in one buffer,
+  // layer 0's q|k|v tables, and the folded q|k|v of the next layer [rows, 3d]
+  struct FoldW {
+    float *wzq, *bzq, *sq, *cq;          // z_q = W_q' y_sa:  [d, 2d] over [attn | x]
+    float *wzh, *bzh, *sh, *ch;          // z_h = W_1' y_ca:  [ff, 2d] over [attn | LN1(y_sa)]
+    float *wzqkv, *bzqkv, *sqkv, *cqkv;  // z_qkv(l+1) = W_in' y_ff: [3d, ff + d] over [hidden | LN2(y_ca)]
+  };
+  std::vector<FoldW> foldw;
+  float* fold_buf = nullptr;
+  float *qtab = nullptr, *qpos = nullptr, *dzqkv = nullptr;
 
   // timing
   bool timing = false;
@@ -340,7 +350,7 @@ struct mocr_engine {
                     ds_sa,   ds_ca,   ds_ff,
                     dlogits_hist, kcache, vcache, ids, feed, forced, finished, logp, st, XWh, XWl, ATTh, ATTl,
                     HIDh, HIDl, MEMh, MEMl, dwh, dwl, kvwh, kvwl, bscore, bfin, bseq[0], bseq[1],
-                    bslot[0], bslot[1]};
+                    bslot[0], bslot[1], fold_buf, qtab, qpos, dzqkv};
     for (void* p : bufs)
       if (p) (void)hipFree(p);
     for (float* p : relbias)
@@ -723,6 +733,36 @@ struct mocr_engine {
         bslot[i] = dalloc<int32_t>(R * ld_ids);
       }
     }
+    if (fold_on) {
+      const size_t ff = cfg.d_ff;
+      const size_t per = 2 * d * d + 3 * d + ff * 2 * d + 3 * ff + 3 * d * (ff + d) + 9 * d;
+      fold_buf = dalloc<float>(per * L);
+      foldw.resize(L);
+      float* f = fold_buf;
+      auto take = [&](size_t n) {
+        float* o = f;
+        f += n;
+        return o;
+      };
+      for (size_t l = 0; l < L; ++l) {
+        FoldW& w = foldw[l];
+        w.wzq = take(2 * d * d);
+        w.bzq = take(d);
+        w.sq = take(d);
+        w.cq = take(d);
+        w.wzh = take(ff * 2 * d);
+        w.bzh = take(ff);
+        w.sh = take(ff);
+        w.ch = take(ff);
+        w.wzqkv = take(3 * d * (ff + d));
+        w.bzqkv = take(3 * d);
+        w.sqkv = take(3 * d);
+        w.cqkv = take(3 * d);
+      }
+      qtab = dalloc<float>((size_t)cfg.vocab * 3 * d);
+      qpos = dalloc<float>((size_t)cfg.max_pos * 3 * d);
+      dzqkv = dalloc<float>(B * 3 * d);
+    }
     ids = dalloc<int32_t>(B * ld_ids);
     feed = dalloc<int32_t>(B * ld_ids);
     forced = dalloc<int32_t>(B * ld_ids);
@@ -804,9 +844,51 @@ struct mocr_engine {
       launch_split_bf16(kvw_all, kvwh, kvwl, (size_t)cfg.n_layers * 2 * d * d, stream);
       MOCR_HIP_CHECK(hipStreamSynchronize(stream));
     }
+    if (fold_on) fold_decoder();
     MOCR_HIP_CHECK(hipDeviceSynchronize());
     weights_loaded = true;
     encoded = false;
+  }
+
+  // Folded greedy-step weights (kernels.h FoldGemmParams), fp64-accumulated on the device.
+  // For a LayerNorm (g, b) in front of W x + c: W' = W diag(g), s = W g, c' = W b + c, and
+  // W' times the producer's terms: z_q over [SA attn | x] = [W_q' W_o | W_q'] + W_q' b_o;
+  // z_h over [CA attn | LN1(y_sa)] = [W_1' W_o | W_1'] + W_1' b_o; the next layer's z_qkv
+  // over [hidden | LN2(y_ca)] = [W_in' W_2 | W_in'] + W_in' b_2.  Layer 0's q|k|v of token
+  // v at position p: qtab[v] + qpos[p] = W_in emb[v] + b_in + W_in pos[p].
+  void fold_decoder() {
+    const int d = cfg.d_model, ff = cfg.d_ff, L = cfg.n_layers;
+    hipStream_t s = stream;
+    for (int l = 0; l < L; ++l) {
+      const DecLayerW& w = lay->layers[l];
+      FoldW& f = foldw[l];
+      const float* wq = W(w.ca_inw);  // q rows of the cross-attention in_proj
+      launch_fold_mm(wq, d, W(w.n1w), W(w.sa_ow), d, 1, d, nullptr, nullptr, f.wzq, 2 * d, d, d, s);
+      launch_fold_mm(wq, d, W(w.n1w), nullptr, 0, 0, 0, nullptr, nullptr, f.wzq + d, 2 * d, d, d, s);
+      launch_fold_mm(wq, d, W(w.n1w), W(w.sa_ob), 1, 0, d, nullptr, nullptr, f.bzq, 1, d, 1, s);
+      launch_fold_mm(wq, d, nullptr, W(w.n1w), 1, 0, d, nullptr, nullptr, f.sq, 1, d, 1, s);
+      launch_fold_mm(wq, d, nullptr, W(w.n1b), 1, 0, d, W(w.ca_inb), nullptr, f.cq, 1, d, 1, s);
+      const float* w1 = W(w.l1w);
+      launch_fold_mm(w1, d, W(w.n2w), W(w.ca_ow), d, 1, d, nullptr, nullptr, f.wzh, 2 * d, ff, d, s);
+      launch_fold_mm(w1, d, W(w.n2w), nullptr, 0, 0, 0, nullptr, nullptr, f.wzh + d, 2 * d, ff, d, s);
+      launch_fold_mm(w1, d, W(w.n2w), W(w.ca_ob), 1, 0, d, nullptr, nullptr, f.bzh, 1, ff, 1, s);
+      launch_fold_mm(w1, d, nullptr, W(w.n2w), 1, 0, d, nullptr, nullptr, f.sh, 1, ff, 1, s);
+      launch_fold_mm(w1, d, nullptr, W(w.n2b), 1, 0, d, W(w.l1b), nullptr, f.ch, 1, ff, 1, s);
+      if (l + 1 < L) {
+        const DecLayerW& nx = lay->layers[l + 1];
+        const float* wi = W(nx.sa_inw);
+        launch_fold_mm(wi, d, W(w.n3w), W(w.l2w), ff, 1, d, nullptr, nullptr, f.wzqkv, ff + d, 3 * d, ff, s);
+        launch_fold_mm(wi, d, W(w.n3w), nullptr, 0, 0, 0, nullptr, nullptr, f.wzqkv + ff, ff + d, 3 * d, d, s);
+        launch_fold_mm(wi, d, W(w.n3w), W(w.l2b), 1, 0, d, nullptr, nullptr, f.bzqkv, 1, 3 * d, 1, s);
+        launch_fold_mm(wi, d, nullptr, W(w.n3w), 1, 0, d, nullptr, nullptr, f.sqkv, 1, 3 * d, 1, s);
+        launch_fold_mm(wi, d, nullptr, W(w.n3b), 1, 0, d, W(nx.sa_inb), nullptr, f.cqkv, 1, 3 * d, 1, s);
+      }
+    }
+    const DecLayerW& l0 = lay->layers[0];
+    launch_fold_mm(W(lay->emb), d, nullptr, W(l0.sa_inw), 1, d, d, nullptr, W(l0.sa_inb), qtab, 3 * d, cfg.vocab,
+                   3 * d, s);
+    launch_fold_mm(W(lay->pos), d, nullptr, W(l0.sa_inw), 1, d, d, nullptr, nullptr, qpos, 3 * d, cfg.max_pos, 3 * d, s);
+    MOCR_HIP_CHECK(hipStreamSynchronize(s));
   }
 
   void set_images(const float* src, int B, hipMemcpyKind kind) {
@@ -876,6 +958,10 @@ struct mocr_engine {
   // measured slower (decode-only, 3 replicas: 2757 vs 3230 img/s); MOCR_DEC_FUSED=1
   // selects it.  Beam search always uses it (slot-table keys, shared image memory).
   const bool fused_attn = getenv("MOCR_DEC_FUSED") != nullptr && atoi(getenv("MOCR_DEC_FUSED")) != 0;
+  // Greedy decoder on the folded step (5 kernels per layer, kernels.h FoldGemmParams);
+  // MOCR_DEC_FOLD=0 selects the 8-kernel step (A/B).
+  const bool fold_on = !(getenv("MOCR_DEC_FOLD") != nullptr && atoi(getenv("MOCR_DEC_FOLD")) == 0);
+  bool fold_greedy() const { return fold_on && !fused_attn; }
   int attn_passes() const {
     return cfg.precision == MOCR_PRECISION_FP32 ? 0 : (cfg.precision == MOCR_PRECISION_BF16X3 ? 3 : 1);
   }
@@ -1029,6 +1115,7 @@ struct mocr_engine {
   void record_layers(int B, int t, const DecodeState* stp, const int32_t* slots, int mem_div) {
     const int d = cfg.d_model, L = cfg.n_layers;
     const bool fused = fused_attn || slots != nullptr || mem_div != 1;
+    if (!fused && fold_greedy()) return record_layers_fold(B, t, stp);
     const size_t cache_layer = (size_t)max_rows * cfg.max_pos * d;
     const size_t kv_layer = (size_t)cfg.max_batch * M * 2 * d;
     hipStream_t s = stream;
@@ -1118,6 +1205,58 @@ struct mocr_engine {
     }
   }
 
+  // The folded greedy step (kernels.h FoldGemmParams): per layer 5 dependent kernels --
+  // self-attention (q|k|v unfolded from dzqkv: layer 0's from the embedding tables, later
+  // layers' from the previous FFN kernel), out_proj + z_q, cross-attention (q unfolded),
+  // out_proj + z_h, FFN (hidden unfolded from z_h) + the next layer's z_qkv.
+  void record_layers_fold(int B, int t, const DecodeState* stp) {
+    const int d = cfg.d_model, L = cfg.n_layers;
+    const size_t cache_layer = (size_t)max_rows * cfg.max_pos * d;
+    const size_t kv_layer = (size_t)cfg.max_batch * M * 2 * d;
+    hipStream_t s = stream;
+    for (int l = 0; l < L; ++l) {
+      const DecLayerW& w = lay->layers[l];
+      const FoldW& f = foldw[l];
+      const DecLayerW* prev = l ? &lay->layers[l - 1] : nullptr;
+      float* kc = kcache + l * cache_layer;
+      float* vc = vcache + l * cache_layer;
+      // y_sa = x + SA(x): attention, then out_proj + z_q = W_q' y_sa
+      FoldAttnParams a{};
+      a.st = stp; a.t = t; a.B = B; a.out = datt; a.z = dzqkv; a.z_ld = 3 * d;
+      if (l) { a.z_stats = ds_ff; a.s = foldw[l - 1].sqkv; a.c = foldw[l - 1].cqkv; }
+      a.K = kc; a.V = vc; a.kcache = kc; a.vcache = vc;
+      a.kv_b_stride = (size_t)cfg.max_pos * d; a.kv_row_stride = d; a.n = t + 1;
+      launch_dec_foldattn(a, true, s);
+      FoldGemmParams g{};
+      g.B = B; g.t = t; g.st = stp;
+      g.A1 = datt; g.K1 = d; g.A2 = l ? dy_ff : dx;
+      if (l) { g.a2_stats = ds_ff; g.a2_g = W(prev->n3w); g.a2_b = W(prev->n3b); }
+      g.Wy = W(w.sa_ow); g.by = W(w.sa_ob); g.y = dy_sa; g.y_stats = ds_sa;
+      g.Wz = f.wzq; g.bz = f.bzq; g.z = dq; g.NZ = d;
+      launch_foldgemm(g, s);
+      // y_ca = LN1(y_sa) + CA(LN1(y_sa), mem): attention, then out_proj + z_h = W_1' y_ca
+      const float* memk = MEMKV + l * kv_layer;
+      a = FoldAttnParams{};
+      a.st = stp; a.t = t; a.B = B; a.out = datt; a.z = dq; a.z_ld = d; a.z_stats = ds_sa; a.s = f.sq; a.c = f.cq;
+      a.K = memk; a.V = memk + d; a.kv_b_stride = (size_t)M * 2 * d; a.kv_row_stride = 2 * d; a.n = M;
+      launch_dec_foldattn(a, false, s);
+      g = FoldGemmParams{};
+      g.B = B; g.t = t; g.st = stp;
+      g.A1 = datt; g.K1 = d; g.A2 = dy_sa; g.a2_stats = ds_sa; g.a2_g = W(w.n1w); g.a2_b = W(w.n1b);
+      g.Wy = W(w.ca_ow); g.by = W(w.ca_ob); g.y = dy_ca; g.y_stats = ds_ca;
+      g.Wz = f.wzh; g.bz = f.bzh; g.z = dh; g.NZ = cfg.d_ff;
+      launch_foldgemm(g, s);
+      // y_ff = LN2(y_ca) + W_2 relu(unfold(z_h)) + b_2, and the next layer's z_qkv
+      g = FoldGemmParams{};
+      g.B = B; g.t = t; g.st = stp;
+      g.A1 = dh; g.K1 = cfg.d_ff; g.a1_stats = ds_ca; g.a1_s = f.sh; g.a1_c = f.ch;
+      g.A2 = dy_ca; g.a2_stats = ds_ca; g.a2_g = W(w.n2w); g.a2_b = W(w.n2b);
+      g.Wy = W(w.l2w); g.by = W(w.l2b); g.y = dy_ff; g.y_stats = ds_ff;
+      if (l + 1 < L) { g.Wz = f.wzqkv; g.bz = f.bzqkv; g.z = dzqkv; g.NZ = 3 * d; }
+      launch_foldgemm(g, s);
+    }
+  }
+
   // Logits of the last layer's LN3 output over `B` rows into `out` (row stride Vpad).
   void record_logits(int B, int t, const DecodeState* stp, float* out, size_t hist_stride) {
     const int d = cfg.d_model, L = cfg.n_layers;
@@ -1150,9 +1289,10 @@ struct mocr_engine {
     float* out = hist ? dlogits_hist : dlogits;
     const size_t hs = hist ? (size_t)cfg.max_batch * Vpad : 0;
     record_logits(B, t, stp, out, hs);
+    const bool fold = fold_greedy();
     launch_dec_argmax(st, t, t + 1 >= max_steps, out, hs, Vpad, cfg.vocab, B, ids, feed, use_forced ? forced : nullptr,
                       ld_ids, logp, finished, cfg.eos_id, stop_batch ? 1 : 0, W(lay->emb), W(lay->pos), dx,
-                      cfg.d_model, stream);
+                      cfg.d_model, stream, fold ? qtab : nullptr, fold ? qpos : nullptr, fold ? dzqkv : nullptr);
   }
 
   BeamParams beam_params(int B, int K, int t, int max_steps, bool stop_batch) {
@@ -1252,7 +1392,9 @@ struct mocr_engine {
     h.done_step = 0x7fffffff;
     h.batch = B;
     MOCR_HIP_CHECK(hipMemcpyAsync(st, &h, sizeof(h), hipMemcpyHostToDevice, stream));
-    launch_dec_embed0(feed, ld_ids, W(lay->emb), W(lay->pos), dx, B, cfg.d_model, stream);
+    const bool fold = fold_greedy();
+    launch_dec_embed0(feed, ld_ids, W(lay->emb), W(lay->pos), dx, B, cfg.d_model, stream, fold ? qtab : nullptr,
+                      fold ? qpos : nullptr, fold ? dzqkv : nullptr);
     const int chunks = (max_steps + kDecodeChunk - 1) / kDecodeChunk;
     DecodeState hs{};
     for (int c = 0; c < chunks; ++c) {

@@ -132,9 +132,68 @@ struct RowGemmParams {
 };
 void launch_rowgemm(const RowGemmParams& p, hipStream_t s);
 
-// x[b] = embedding[feed[b][0]] + pos[0] and DecodeState init (outside the graph).
+// ------------------------------------------------------------------ folded greedy step
+// The post-norm LayerNorm in front of each projection is folded into the producer of its
+// input (engine.hip fold_decoder, decfold.hip): for LN(y) = g (y - mu) rstd + b feeding
+// W x + c, W LN(y) + c = rstd (W' y - mu s) + c' with W' = W diag(g), s = W g,
+// c' = W b + c, and W' y is expanded over y's own terms (residual + projection), so it
+// is one more column block of y's producer.  The consumer applies rstd and mu (y's slice
+// statistics), s and c' when it loads z = W' y.
+//
+// Fold row GEMM over A = [A1 (K1 columns) | A2 (d columns)]:
+//   A1' = A1, or relu(rstd (A1 - mu s) + c) with the statistics a1_stats (the FFN hidden)
+//   A2' = A2 (embedding), or LN(A2) with a2_stats, a2_g, a2_b (the sublayer input)
+//   y[:, 0:d)  = A2' + (Wy A1' + by), and y's slice statistics      (pre-norm sum)
+//   z[:, 0:NZ) = Wz [A1' | A2'] + bz                                 (next projection, folded)
+struct FoldGemmParams {
+  const float* A1;
+  int K1;
+  const float *a1_stats, *a1_s, *a1_c;
+  const float* A2;
+  const float *a2_stats, *a2_g, *a2_b;
+  const float *Wy, *by;
+  float *y, *y_stats;
+  const float *Wz, *bz;
+  float* z;
+  int NZ;
+  int B, t;
+  const DecodeState* st;
+};
+void launch_foldgemm(const FoldGemmParams& p, hipStream_t s);
+
+// Attention of the newest position with folded inputs, one workgroup per (row, head):
+// q = rstd (z_q - mu s) + c from z [B, z_ld] and z_stats (plain z when z_stats is null).
+// Self-attention: z holds q|k|v (s, c: [3d]); the new k/v are appended to the cache at t
+// and the keys are cache rows 0..t.  Cross-attention: K/V = the memory K/V, n = M.
+struct FoldAttnParams {
+  const DecodeState* st;
+  int t;
+  const float* z;
+  int z_ld;
+  const float *z_stats, *s, *c;
+  const float* K;
+  const float* V;
+  float *kcache, *vcache;  // self only: this layer's cache (same strides as K/V)
+  size_t kv_b_stride;
+  int kv_row_stride;
+  int n;                   // keys (self: t + 1)
+  float* out;              // [B, d]
+  int B;
+};
+void launch_dec_foldattn(const FoldAttnParams& p, bool self_attn, hipStream_t s);
+
+// out[i, j] = sum_k A[i, k] g[k] Bm[k*sbk + j*sbj] + add_row[i] + add_col[j], accumulated in
+// fp64 and rounded once (g null: 1; Bm null: out = A diag(g), K unused).  Load-time
+// weight folding only.
+void launch_fold_mm(const float* A, int lda, const float* g, const float* Bm, long sbk, long sbj, int K,
+                    const float* add_row, const float* add_col, float* out, int ldo, int rows, int cols,
+                    hipStream_t s);
+
+// x[b] = embedding[feed[b][0]] + pos[0] and DecodeState init (outside the graph).  With
+// qtab: z[b] = qtab[feed[b][0]] + qpos[0], the first layer's folded q|k|v ([V, 3d] and
+// [max_pos, 3d] tables).
 void launch_dec_embed0(const int32_t* feed, int ld_ids, const float* emb, const float* pos, float* x, int B, int d,
-                       hipStream_t s);
+                       hipStream_t s, const float* qtab = nullptr, const float* qpos = nullptr, float* z = nullptr);
 
 // Attention of the newest position over n keys (self: n = t+1 from the KV cache;
 // cross: n = M memory tokens).  K/V rows for image b start at K + b*kv_b_stride.
@@ -200,6 +259,7 @@ void launch_dec_attn(const DecodeState* st, int t, const float* q, const float* 
 void launch_dec_argmax(DecodeState* st, int t, int last_step, const float* logits, size_t hist_stride, int ldl,
                        int V, int B, int32_t* ids, int32_t* feed, const int32_t* forced, int ld_ids, float* logp,
                        int32_t* finished, int eos, int stop_batch, const float* emb, const float* pos, float* x,
-                       int d, hipStream_t s);
+                       int d, hipStream_t s, const float* qtab = nullptr, const float* qpos = nullptr,
+                       float* z = nullptr);
 
 }  // namespace mocr

@@ -38,7 +38,7 @@ int main() {
   float* att = alloc<float>(B * d);
   float* W = alloc<float>((size_t)Vp * 512);
   float* bias = alloc<float>(Vp);
-  float* g = alloc<float>(512);
+  float* g = alloc<float>(1024);
   float* kc = alloc<float>((size_t)B * P * d);
   float* vc = alloc<float>((size_t)B * P * d);
   float* memkv = alloc<float>((size_t)L * B * M * 2 * d);
@@ -66,6 +66,17 @@ int main() {
       launch_rowgemm(p, ss);
     };
   };
+  float* zb = alloc<float>(B * 768);
+  float* wz = alloc<float>((size_t)768 * 768);
+  auto fg = [&](int K1, int NZ, bool s1) {
+    return [=](hipStream_t ss) {
+      FoldGemmParams p{};
+      p.B = B; p.t = t; p.A1 = x; p.K1 = K1; p.A2 = q; p.a2_stats = stats; p.a2_g = g; p.a2_b = g;
+      if (s1) { p.a1_stats = stats; p.a1_s = g; p.a1_c = g; }
+      p.Wy = W; p.by = bias; p.y = y; p.y_stats = stats2; p.Wz = wz; p.bz = bias; p.z = zb; p.NZ = NZ;
+      launch_foldgemm(p, ss);
+    };
+  };
   std::vector<std::pair<std::string, std::function<void(hipStream_t)>>> cases = {
       {"qkv N768 K256 +LN(A)", rg(DEC_QKV, 768, 256, true, false)},
       {"oproj N256 K256 +LN(res)", rg(DEC_RESADD, 256, 256, false, true)},
@@ -83,6 +94,26 @@ int main() {
       {"argmax+embed", [=](hipStream_t ss) {
          launch_dec_argmax(st, t, 0, logits, 0, Vp, V, B, ids, feed, nullptr, 151, logp, fin, 2, 0, W, W, x, d, ss);
        }},
+      {"argmax+embed+qkv table", [=](hipStream_t ss) {
+         launch_dec_argmax(st, t, 0, logits, 0, Vp, V, B, ids, feed, nullptr, 151, logp, fin, 2, 0, W, W, x, d, ss,
+                           W, W, zb);
+       }},
+      {"fold self-attn t=100", [=](hipStream_t ss) {
+         FoldAttnParams a{};
+         a.t = t; a.B = B; a.out = att; a.z = zb; a.z_ld = 3 * d; a.z_stats = stats; a.s = g; a.c = g;
+         a.K = kc; a.V = vc; a.kcache = kc; a.vcache = vc; a.kv_b_stride = (size_t)P * d; a.kv_row_stride = d;
+         a.n = t + 1;
+         launch_dec_foldattn(a, true, ss);
+       }},
+      {"fold cross-attn M=144", [=](hipStream_t ss) {
+         FoldAttnParams a{};
+         a.t = t; a.B = B; a.out = att; a.z = zb; a.z_ld = d; a.z_stats = stats; a.s = g; a.c = g;
+         a.K = memkv; a.V = memkv + d; a.kv_b_stride = (size_t)M * 2 * d; a.kv_row_stride = 2 * d; a.n = M;
+         launch_dec_foldattn(a, false, ss);
+       }},
+      {"foldgemm y256+z256 K1=256 +LN", fg(256, 256, false)},
+      {"foldgemm y256+z512 K1=256 +LN", fg(256, 512, false)},
+      {"foldgemm y256+z768 K1=512 +unf", fg(512, 768, true)},
   };
   const int chain = 200;
   for (auto& c : cases) {
