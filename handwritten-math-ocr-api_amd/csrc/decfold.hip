@@ -16,6 +16,8 @@
 // Loads are never predicated per element: out-of-range rows / keys read a clamped valid
 // address and are masked after the load (hipcc turns `c ? *p : 0` into a branch and a
 // full vmcnt(0) wait per element).
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace mocr {
@@ -86,9 +88,9 @@ __device__ __forceinline__ void row_stats_16lanes(const float* __restrict__ part
 // DEC_RESADD (y = A2' + (acc + by), then the (mean, M2) of the tile's 16 columns).  The
 // 16-wide k chunks never straddle A1 / A2 (K1 % 16 == 0), so a chunk's source is
 // wave-uniform.  S1 / S2: A1 / A2 carry statistics (unfold / LayerNorm on load).
-template <int NI, bool YT, bool S1, bool S2>
+template <int NI, bool YT, bool S1, bool S2, int NW>
 __device__ __forceinline__ void fold_tile(const FoldGemmParams& p, int c0) {
-  __shared__ float red[4][16][17];
+  __shared__ float red[NW][16][17];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -159,13 +161,16 @@ __device__ __forceinline__ void fold_tile(const FoldGemmParams& p, int c0) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) red[wave][g * 4 + r][lane & 15] = acc[r];
   __syncthreads();
+  if (tid >= 256) return;  // 16 x 16 outputs: the first 4 waves
   if constexpr (YT && S2) {  // all 16 lanes of a row take part in the merge
     float mean, rstd;
     row_stats_16lanes(p.a2_stats + (size_t)rrow * 2 * kSlices, col, mean, rstd);
     rres = ln_apply(rres, mean, rstd, rg, rb);
   }
   if (grow >= p.B || dec_skip(p.st, p.t)) return;  // uniform per 16-lane row group
-  const float val = ((red[0][row][col] + red[1][row][col]) + red[2][row][col]) + red[3][row][col];
+  float val = red[0][row][col];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) val += red[w][row][col];
   if constexpr (YT) {
     const float y = rres + (val + p.by[gcol]);
     p.y[(size_t)grow * kD + gcol] = y;
@@ -190,12 +195,13 @@ __device__ __forceinline__ void fold_tile(const FoldGemmParams& p, int c0) {
   }
 }
 
-template <int K1, bool S1, bool S2>
-__global__ void __launch_bounds__(256) foldgemm_kernel(FoldGemmParams p) {
+// NW waves split K (4 or 8: 512-thread workgroups halve each wave's load chain).
+template <int K1, bool S1, bool S2, int NW>
+__global__ void __launch_bounds__(64 * NW) foldgemm_kernel(FoldGemmParams p) {
   if (blockIdx.x < kD / 16)
-    fold_tile<K1 / 64, true, S1, S2>(p, blockIdx.x * 16);
+    fold_tile<K1 / (16 * NW), true, S1, S2, NW>(p, blockIdx.x * 16);
   else
-    fold_tile<(K1 + kD) / 64, false, S1, S2>(p, (blockIdx.x - kD / 16) * 16);
+    fold_tile<(K1 + kD) / (16 * NW), false, S1, S2, NW>(p, (blockIdx.x - kD / 16) * 16);
 }
 
 // ------------------------------------------------------------------ fold attention
@@ -370,14 +376,22 @@ void launch_foldgemm(const FoldGemmParams& p, hipStream_t s) {
   if (!p.A1 || !p.A2 || !p.Wy || !p.by || !p.y || !p.y_stats) throw std::runtime_error("foldgemm: null operand");
   if (p.B <= 0) return;
   const dim3 grid(kD / 16 + p.NZ / 16, (p.B + 15) / 16);
-  if (p.K1 == 256 && !s1 && !s2)
-    foldgemm_kernel<256, false, false><<<grid, 256, 0, s>>>(p);
-  else if (p.K1 == 256 && !s1 && s2)
-    foldgemm_kernel<256, false, true><<<grid, 256, 0, s>>>(p);
-  else if (p.K1 == 512 && s1 && s2)
-    foldgemm_kernel<512, true, true><<<grid, 256, 0, s>>>(p);
-  else
+  static const int nw = getenv("MOCR_FOLD_WAVES") ? atoi(getenv("MOCR_FOLD_WAVES")) : 4;
+#define MOCR_FG(K1, S1, S2)                                                     \
+  if (nw == 8)                                                                  \
+    foldgemm_kernel<K1, S1, S2, 8><<<grid, 512, 0, s>>>(p);                     \
+  else                                                                          \
+    foldgemm_kernel<K1, S1, S2, 4><<<grid, 256, 0, s>>>(p);
+  if (p.K1 == 256 && !s1 && !s2) {
+    MOCR_FG(256, false, false)
+  } else if (p.K1 == 256 && !s1 && s2) {
+    MOCR_FG(256, false, true)
+  } else if (p.K1 == 512 && s1 && s2) {
+    MOCR_FG(512, true, true)
+  } else {
     throw std::runtime_error("foldgemm: built for (K1 256, A2 plain or LayerNorm) and (K1 512, both)");
+  }
+#undef MOCR_FG
   MOCR_HIP_CHECK(hipGetLastError());
 }
 

@@ -162,6 +162,32 @@ __global__ void __launch_bounds__(256) rowgemm_kernel(RowGemmParams p) {
     row_stats_16lanes(p.r_stats + (size_t)(grow < p.B ? grow : 0) * 2 * kSlices, col, mean, rstd);
     rres = ln_apply(rres, mean, rstd, rg, rb);
   }
+  if constexpr (EPI == DEC_LOGITS) {
+    if (grow >= p.B || dec_skip(p.st, t)) return;  // uniform per 16-lane row group
+    const bool cv = gcol < p.n_valid;
+    const float v = (((red[0][row][col] + red[1][row][col]) + red[2][row][col]) + red[3][row][col]) + p.bias[gcol];
+    if (cv) p.out[(p.hist_stride ? (size_t)t * p.hist_stride : 0) + (size_t)grow * p.ldo + gcol] = v;
+    if (p.part) {
+      // the tile's (max, first argmax, sum exp(l - max)) over its 16 columns of the row
+      float m = cv ? v : -INFINITY;
+      int ix = gcol;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const float om = __shfl_xor(m, o, 64);
+        const int oi = __shfl_xor(ix, o, 64);
+        if (om > m || (om == m && oi < ix)) {
+          m = om;
+          ix = oi;
+        }
+      }
+      float e = cv ? expf(v - m) : 0.f;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) e += __shfl_xor(e, o, 64);
+      if (col == 0)
+        reinterpret_cast<floatx4*>(p.part)[(size_t)grow * gridDim.x + blockIdx.x] = floatx4{m, __int_as_float(ix), e, 0.f};
+    }
+    return;
+  }
   if (!out_ok || dec_skip(p.st, t)) return;  // uniform per 16-lane row group
   float v = ((red[0][row][col] + red[1][row][col]) + red[2][row][col]) + red[3][row][col];
   v += p.bias[gcol];
@@ -197,9 +223,6 @@ __global__ void __launch_bounds__(256) rowgemm_kernel(RowGemmParams p) {
     } else {
       p.vcache[((size_t)grow * p.max_pos + t) * p.d + (gcol - 2 * p.d)] = v;
     }
-  } else {  // DEC_LOGITS
-    float* slot = p.out + (p.hist_stride ? (size_t)t * p.hist_stride : 0);
-    slot[(size_t)grow * p.ldo + gcol] = v;
   }
 }
 
@@ -758,7 +781,8 @@ __global__ void __launch_bounds__(256) dec_argmax_kernel(DecodeState* st, int t,
                                                          int eos, int stop_batch, const float* __restrict__ emb,
                                                          const float* __restrict__ pos, float* __restrict__ x,
                                                          int d, const float* __restrict__ qtab,
-                                                         const float* __restrict__ qpos, float* __restrict__ z) {
+                                                         const float* __restrict__ qpos, float* __restrict__ z,
+                                                         const float* __restrict__ part, int nparts) {
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -767,8 +791,25 @@ __global__ void __launch_bounds__(256) dec_argmax_kernel(DecodeState* st, int t,
   // one pass: running (max, first argmax, Σ exp(l - max)) per thread, then merged
   float best = -INFINITY, sum = 0.f;
   int bidx = 0x7fffffff;
+  auto merge = [](float& b1, int& i1, float& s1, float b2, int i2, float s2) {
+    const float m = fmaxf(b1, b2);
+    const float f1 = b1 == -INFINITY ? 0.f : expf(b1 - m);
+    const float f2 = b2 == -INFINITY ? 0.f : expf(b2 - m);
+    s1 = s1 * f1 + s2 * f2;
+    if (b2 > b1 || (b2 == b1 && i2 < i1)) i1 = i2;
+    b1 = m;
+  };
   constexpr int CH = 20;  // loads in flight per thread: one round for V <= 5120
-  for (int j0 = tid; j0 < V; j0 += 256 * CH) {
+  if (part) {  // per-16-column-tile partials of the logits kernel: 2 per thread for V <= 8192
+    const floatx4* P = reinterpret_cast<const floatx4*>(part) + (size_t)b * nparts;
+    floatx4 q[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) q[c] = P[min(tid + 256 * c, nparts - 1)];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      if (tid + 256 * c < nparts) merge(best, bidx, sum, q[c][0], __float_as_int(q[c][1]), q[c][2]);
+  }
+  for (int j0 = part ? V : tid; j0 < V; j0 += 256 * CH) {
     float vals[CH];
     // unpredicated loads (a clamped column), masked after: a predicated load per element
     // becomes a branch + vmcnt(0) each
@@ -788,14 +829,6 @@ __global__ void __launch_bounds__(256) dec_argmax_kernel(DecodeState* st, int t,
       }
     }
   }
-  auto merge = [](float& b1, int& i1, float& s1, float b2, int i2, float s2) {
-    const float m = fmaxf(b1, b2);
-    const float f1 = b1 == -INFINITY ? 0.f : expf(b1 - m);
-    const float f2 = b2 == -INFINITY ? 0.f : expf(b2 - m);
-    s1 = s1 * f1 + s2 * f2;
-    if (b2 > b1 || (b2 == b1 && i2 < i1)) i1 = i2;
-    b1 = m;
-  };
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float ob = __shfl_xor(best, o, 64);
@@ -896,9 +929,11 @@ void launch_dec_attn(const DecodeState* st, int t, const float* q, const float* 
 void launch_dec_argmax(DecodeState* st, int t, int last_step, const float* logits, size_t hist_stride, int ldl,
                        int V, int B, int32_t* ids, int32_t* feed, const int32_t* forced, int ld_ids, float* logp,
                        int32_t* finished, int eos, int stop_batch, const float* emb, const float* pos, float* x,
-                       int d, hipStream_t s, const float* qtab, const float* qpos, float* z) {
+                       int d, hipStream_t s, const float* qtab, const float* qpos, float* z, const float* part) {
+  const int nparts = ldl / 16;
+  if (part && nparts > 512) throw std::runtime_error("argmax: at most 8192 logits with tile partials");
   dec_argmax_kernel<<<B, 256, 0, s>>>(st, t, last_step, logits, hist_stride, ldl, V, ids, feed, forced, ld_ids, logp,
-                                      finished, eos, stop_batch, emb, pos, x, d, qtab, qpos, z);
+                                      finished, eos, stop_batch, emb, pos, x, d, qtab, qpos, z, part, nparts);
   MOCR_HIP_CHECK(hipGetLastError());
 }
 

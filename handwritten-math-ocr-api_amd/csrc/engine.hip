@@ -329,6 +329,7 @@ struct mocr_engine {
   std::vector<FoldW> foldw;
   float* fold_buf = nullptr;
   float *qtab = nullptr, *qpos = nullptr, *dzqkv = nullptr;
+  float* dpart = nullptr;  // greedy: logits tile partials [rows][Vpad/16] float4 for the argmax
 
   // timing
   bool timing = false;
@@ -350,7 +351,7 @@ struct mocr_engine {
                     ds_sa,   ds_ca,   ds_ff,
                     dlogits_hist, kcache, vcache, ids, feed, forced, finished, logp, st, XWh, XWl, ATTh, ATTl,
                     HIDh, HIDl, MEMh, MEMl, dwh, dwl, kvwh, kvwl, bscore, bfin, bseq[0], bseq[1],
-                    bslot[0], bslot[1], fold_buf, qtab, qpos, dzqkv};
+                    bslot[0], bslot[1], fold_buf, qtab, qpos, dzqkv, dpart};
     for (void* p : bufs)
       if (p) (void)hipFree(p);
     for (float* p : relbias)
@@ -722,6 +723,7 @@ struct mocr_engine {
     ds_ff = dalloc<float>(R * 32);
     dh = dalloc<float>(R * cfg.d_ff);
     dlogits = dalloc<float>(R * Vpad);
+    dpart = dalloc<float>(B * Vpad / 4);
     kcache = dalloc<float>(L * R * cfg.max_pos * d);
     vcache = dalloc<float>(L * R * cfg.max_pos * d);
     ld_ids = cfg.max_pos + 1;
@@ -1258,7 +1260,7 @@ struct mocr_engine {
   }
 
   // Logits of the last layer's LN3 output over `B` rows into `out` (row stride Vpad).
-  void record_logits(int B, int t, const DecodeState* stp, float* out, size_t hist_stride) {
+  void record_logits(int B, int t, const DecodeState* stp, float* out, size_t hist_stride, float* part = nullptr) {
     const int d = cfg.d_model, L = cfg.n_layers;
     const DecLayerW& last = lay->layers[L - 1];
     RowGemmParams p{};
@@ -1280,6 +1282,7 @@ struct mocr_engine {
     p.ldo = Vpad;
     p.n_valid = cfg.vocab;
     p.epi = DEC_LOGITS;
+    p.part = part;
     launch_rowgemm(p, stream);
   }
 
@@ -1288,11 +1291,12 @@ struct mocr_engine {
     record_layers(B, t, stp, nullptr, 1);
     float* out = hist ? dlogits_hist : dlogits;
     const size_t hs = hist ? (size_t)cfg.max_batch * Vpad : 0;
-    record_logits(B, t, stp, out, hs);
+    record_logits(B, t, stp, out, hs, dpart);
     const bool fold = fold_greedy();
     launch_dec_argmax(st, t, t + 1 >= max_steps, out, hs, Vpad, cfg.vocab, B, ids, feed, use_forced ? forced : nullptr,
                       ld_ids, logp, finished, cfg.eos_id, stop_batch ? 1 : 0, W(lay->emb), W(lay->pos), dx,
-                      cfg.d_model, stream, fold ? qtab : nullptr, fold ? qpos : nullptr, fold ? dzqkv : nullptr);
+                      cfg.d_model, stream, fold ? qtab : nullptr, fold ? qpos : nullptr, fold ? dzqkv : nullptr,
+                      dpart);
   }
 
   BeamParams beam_params(int B, int K, int t, int max_steps, bool stop_batch) {

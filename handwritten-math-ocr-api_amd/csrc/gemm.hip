@@ -279,10 +279,12 @@ __device__ __forceinline__ void epi_store16(const GemmParams& p, int row, int co
 
 // GELU for the bf16 / bf16x3 epilogues: erf by Abramowitz & Stegun 7.1.26 (one
 // reciprocal, one exp, 6 FMAs, no branches; |erf error| <= 1.5e-7, two orders below the
-// bf16x3 products' ~1e-5).  The fp32 path keeps the library erff (gelu_erf).
+// bf16x3 products' ~1e-5).  The fp32 path keeps the library erff (gelu_erf).  The
+// reciprocal is the 1-ulp v_rcp_f32: __frcp_rn expands to the ~10-instruction IEEE
+// division sequence, which made this epilogue cost a fifth of s3.fc1's time.
 __device__ __forceinline__ float gelu_fast(float x) {
   const float z = fabsf(x) * 0.70710678118654752440f;
-  const float t = __frcp_rn(fmaf(0.3275911f, z, 1.0f));
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
   float poly = fmaf(1.061405429f, t, -1.453152027f);
   poly = fmaf(poly, t, 1.421413741f);
   poly = fmaf(poly, t, -0.284496736f);

@@ -126,6 +126,7 @@ struct RowGemmParams {
   int d, max_pos;
   int n_valid;         // columns < n_valid are real (fc_out padding)
   size_t hist_stride;  // DEC_LOGITS: floats between step slots (0: single slot)
+  float* part;         // DEC_LOGITS (nullable): per row and 16-column tile {max, argmax bits, sum exp(l - max), 0}
   int epi;
   int t;               // decode step
   const DecodeState* st;
@@ -255,11 +256,12 @@ void launch_dec_attn(const DecodeState* st, int t, const float* q, const float* 
                      size_t kv_b_stride, int kv_row_stride, int n_fixed, int n_max, float* out, int B, int d,
                      int heads, hipStream_t s, int q_ld = 0, int kv_mod = 0);
 
-// Argmax + log-prob + finish flags + next fed token + next step's embedding.
+// Argmax + log-prob + finish flags + next fed token + next step's embedding.  With `part`
+// (the logits kernel's tile partials [B][ldl/16] float4) the logits are not re-read.
 void launch_dec_argmax(DecodeState* st, int t, int last_step, const float* logits, size_t hist_stride, int ldl,
                        int V, int B, int32_t* ids, int32_t* feed, const int32_t* forced, int ld_ids, float* logp,
                        int32_t* finished, int eos, int stop_batch, const float* emb, const float* pos, float* x,
                        int d, hipStream_t s, const float* qtab = nullptr, const float* qpos = nullptr,
-                       float* z = nullptr);
+                       float* z = nullptr, const float* part = nullptr);
 
 }  // namespace mocr

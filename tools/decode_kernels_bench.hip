@@ -67,6 +67,7 @@ int main() {
     };
   };
   float* zb = alloc<float>(B * 768);
+  float* part = alloc<float>(B * Vp / 4);
   float* wz = alloc<float>((size_t)768 * 768);
   auto fg = [&](int K1, int NZ, bool s1) {
     return [=](hipStream_t ss) {
@@ -94,6 +95,17 @@ int main() {
       {"argmax+embed", [=](hipStream_t ss) {
          launch_dec_argmax(st, t, 0, logits, 0, Vp, V, B, ids, feed, nullptr, 151, logp, fin, 2, 0, W, W, x, d, ss);
        }},
+      {"logits + tile partials", [=](hipStream_t ss) {
+         RowGemmParams p{};
+         p.A = x; p.W = W; p.bias = bias; p.out = logits; p.B = B; p.N = Vp; p.K = d; p.ldo = Vp; p.d = d;
+         p.max_pos = P; p.n_valid = V; p.epi = DEC_LOGITS; p.t = t; p.a_ln_g = g; p.a_ln_b = g; p.a_stats = stats;
+         p.part = part;
+         launch_rowgemm(p, ss);
+       }},
+      {"argmax (tile partials)+qkv", [=](hipStream_t ss) {
+         launch_dec_argmax(st, t, 0, logits, 0, Vp, V, B, ids, feed, nullptr, 151, logp, fin, 2, 0, W, W, x, d, ss,
+                           W, W, zb, part);
+       }},
       {"argmax+embed+qkv table", [=](hipStream_t ss) {
          launch_dec_argmax(st, t, 0, logits, 0, Vp, V, B, ids, feed, nullptr, 151, logp, fin, 2, 0, W, W, x, d, ss,
                            W, W, zb);
@@ -101,6 +113,13 @@ int main() {
       {"fold self-attn t=100", [=](hipStream_t ss) {
          FoldAttnParams a{};
          a.t = t; a.B = B; a.out = att; a.z = zb; a.z_ld = 3 * d; a.z_stats = stats; a.s = g; a.c = g;
+         a.K = kc; a.V = vc; a.kcache = kc; a.vcache = vc; a.kv_b_stride = (size_t)P * d; a.kv_row_stride = d;
+         a.n = t + 1;
+         launch_dec_foldattn(a, true, ss);
+       }},
+      {"fold self-attn t=100 plain z", [=](hipStream_t ss) {
+         FoldAttnParams a{};
+         a.t = t; a.B = B; a.out = att; a.z = zb; a.z_ld = 3 * d;
          a.K = kc; a.V = vc; a.kcache = kc; a.vcache = vc; a.kv_b_stride = (size_t)P * d; a.kv_row_stride = d;
          a.n = t + 1;
          launch_dec_foldattn(a, true, ss);
