@@ -43,7 +43,8 @@ def parse():
     ap.add_argument("--image", type=int, nargs=2, default=[384, 384])
     ap.add_argument("--tokens", type=int, default=128)
     ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3", "bf16"])
-    ap.add_argument("--replicas", type=int, default=3, help="engine replicas pipelining batches per GPU")
+    ap.add_argument("--replicas", type=int, default=4,
+                    help="engine replicas pipelining batches per GPU (throughput plateaus at 4-6: tools/pipeline_probe.py)")
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     ap.add_argument("--cpu-sample", type=int, default=32, help="images in the CPU-baseline sample")
