@@ -964,6 +964,9 @@ struct mocr_engine {
   // MOCR_DEC_FOLD=0 selects the 8-kernel step (A/B).
   const bool fold_on = !(getenv("MOCR_DEC_FOLD") != nullptr && atoi(getenv("MOCR_DEC_FOLD")) == 0);
   bool fold_greedy() const { return fold_on && !fused_attn; }
+  // Encoder: norm2 + MLP fused for the stages mlp.hip is built for (bf16 modes);
+  // MOCR_MLP_FUSED=0 selects the separate LayerNorm / fc1 / fc2 kernels (A/B).
+  const bool mlp_fused = !(getenv("MOCR_MLP_FUSED") != nullptr && atoi(getenv("MOCR_MLP_FUSED")) == 0);
   int attn_passes() const {
     return cfg.precision == MOCR_PRECISION_FP32 ? 0 : (cfg.precision == MOCR_PRECISION_BF16X3 ? 3 : 1);
   }
@@ -1035,6 +1038,7 @@ struct mocr_engine {
     static const char* mrg_n[] = {"merge1", "merge2", "merge3"};
     static const char* ln1_n[] = {"s1.ln1", "s2.ln1", "s3.ln1", "s4.ln1"};
     static const char* ln2_n[] = {"s1.ln2", "s2.ln2", "s3.ln2", "s4.ln2"};
+    static const char* mlp_n[] = {"s1.mlp", "s2.mlp", "s3.mlp", "s4.mlp"};
     static const char* mln_n[] = {"merge1.ln", "merge2.ln", "merge3.ln"};
     const bool b16 = bf16_mode();
     // GEMM A operands: fp32 buffers, or their bf16 planes
@@ -1060,12 +1064,30 @@ struct mocr_engine {
         });
         gemm(proj_n[s], opATT, wop(w.projw), W(w.projb), X, nullptr, nullptr, (int)wrows, C, C, EPI_WINRES, &wg,
              rows);
-        timed(ln2_n[s], 0, 8.0 * rows * C,
-              [&] { launch_layernorm(X, W(w.n2w), W(w.n2b), xw32, XWh, XWl, (int)rows, C, stream); });
-        gemm(fc1_n[s], opXW, wop(w.fc1w), W(w.fc1b), hid32, HIDh, HIDl, (int)rows, 4 * C, C, EPI_GELU, nullptr,
-             rows);
-        gemm(fc2_n[s], opHID, wop(w.fc2w), W(w.fc2b), X, nullptr, nullptr, (int)rows, C, 4 * C, EPI_RESADD, nullptr,
-             rows);
+        if (b16 && mlp_fused && mlp_fused_supported(C)) {
+          // norm2 + fc1 + GELU + fc2 + residual in one kernel (mlp.hip)
+          MlpParams mp{};
+          mp.X = X;
+          mp.M = rows;
+          mp.C = C;
+          mp.ln_g = W(w.n2w);
+          mp.ln_b = W(w.n2b);
+          mp.w1 = dwh + w.fc1w;
+          mp.w1lo = dwl ? dwl + w.fc1w : nullptr;
+          mp.b1 = W(w.fc1b);
+          mp.w2 = dwh + w.fc2w;
+          mp.w2lo = dwl ? dwl + w.fc2w : nullptr;
+          mp.b2 = W(w.fc2b);
+          timed(mlp_n[s], 16.0 * rows * C * C, 8.0 * rows * C + (dwl ? 4.0 : 2.0) * 8.0 * C * C,
+                [&] { launch_mlp_fused(mp, stream); });
+        } else {
+          timed(ln2_n[s], 0, 8.0 * rows * C,
+                [&] { launch_layernorm(X, W(w.n2w), W(w.n2b), xw32, XWh, XWl, (int)rows, C, stream); });
+          gemm(fc1_n[s], opXW, wop(w.fc1w), W(w.fc1b), hid32, HIDh, HIDl, (int)rows, 4 * C, C, EPI_GELU, nullptr,
+               rows);
+          gemm(fc2_n[s], opHID, wop(w.fc2w), W(w.fc2b), X, nullptr, nullptr, (int)rows, C, 4 * C, EPI_RESADD,
+               nullptr, rows);
+        }
       }
       if (stop_after == 1 + 2 * s) return finish_partial(1 + 2 * s);
       if (s < kStages - 1) {

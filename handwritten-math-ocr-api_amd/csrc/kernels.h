@@ -95,6 +95,21 @@ void launch_window_attention(const float* QKV, const float* relbias, const float
 void launch_merge_ln(const float* X, const float* g, const float* b, float* Y, uint16_t* Yh, uint16_t* Yl, int B,
                      int H, int W, int C, hipStream_t s);
 
+// Fused norm2 + MLP + residual of a Swin block (mlp.hip): X[r] += W2 gelu(W1 LN(X[r]) + b1)
+// + b2 on bf16 (w*lo null) or bf16x3 MFMA, the 4C-wide hidden kept on chip.  C = 96, 192.
+struct MlpParams {
+  float* X;                 // [M, C] fp32 residual stream, updated in place
+  long M;
+  int C;
+  const float *ln_g, *ln_b; // norm2
+  const void *w1, *w1lo;    // [4C, C] bf16 hi / lo planes
+  const float* b1;          // [4C]
+  const void *w2, *w2lo;    // [C, 4C]
+  const float* b2;          // [C]
+};
+bool mlp_fused_supported(int C);
+void launch_mlp_fused(const MlpParams& p, hipStream_t s);
+
 // x -> bf16 hi (and lo) planes.
 void launch_split_bf16(const float* x, uint16_t* hi, uint16_t* lo, size_t n, hipStream_t s);
 

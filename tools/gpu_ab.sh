@@ -1,9 +1,16 @@
 #!/bin/bash
-# GPU tests + GEMM A/B (run from the repo root on the GPU box); ring depths as args
+# GPU tests, then the headline bench under environment variants: tools/gpu_ab.sh TAG "ENV=.." ...
 set -e
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests.log 2>&1
-for r in "$@"; do
-  MOCR_GEMM_RING=$r timeout -k 10 180 python tools/gemm_ab.py --precision bf16x3 >> gpurun_out/ab.log 2>&1
-  MOCR_GEMM_RING=$r timeout -k 10 180 python tools/gemm_ab.py --precision bf16 >> gpurun_out/ab.log 2>&1
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+TAG=$1
+shift
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  > gpurun_out/tests_$TAG.log 2>&1
+i=0
+for v in "$@"; do
+  i=$((i+1))
+  env $v timeout -k 10 600 python bench.py --no-cpu-baseline > gpurun_out/bench_${TAG}_$i.json 2>> gpurun_out/bench_$TAG.err
+  echo "$i $v" >> gpurun_out/bench_${TAG}_index.txt
 done
+echo done
