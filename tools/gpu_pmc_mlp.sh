@@ -1,0 +1,12 @@
+#!/bin/bash
+# SQ counters for the encoder kernels (one encode): which limits the fused MLP.
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 60 rocprofv3 -L > gpurun_out/pmc_list.txt 2>&1 || true
+i=0
+for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_MFMA" \
+           "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU SQ_ACTIVE_INST_MISC"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmcm/$i -o run -- python3 tools/profile_encoder.py > gpurun_out/pmcm_$i.log 2>&1 || echo "pass $i failed" >> gpurun_out/pmcm_fail.txt
+done
+exit 0
