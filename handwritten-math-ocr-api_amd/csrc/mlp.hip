@@ -19,8 +19,6 @@
 // The W1 / W2 chunks are staged global -> registers -> LDS (16 B per lane; the 16-B
 // chunks of each row XOR-swizzled so the fragment reads are conflict-free),
 // double-buffered: chunk j+1 is loaded while chunk j runs, one barrier per chunk.
-#include <cstdlib>
-
 #include "kernels.h"
 
 namespace mocr {
@@ -109,7 +107,7 @@ __device__ __forceinline__ int mlp_piece_dst(int k, int wave, int lane) {
   return in1 ? q * W1B + sl * 16 : PL * W1B + q * W2B + sl * 16;
 }
 
-template <int C, int TT, int NC, int PASSES, int EXP = 0>
+template <int C, int TT, int NC, int PASSES>
 __global__ void __launch_bounds__(512) mlp_fused_kernel(MlpParams p) {
   constexpr bool X3 = PASSES == 3;
   constexpr int PL = X3 ? 2 : 1;
@@ -274,13 +272,8 @@ __global__ void __launch_bounds__(512) mlp_fused_kernel(MlpParams p) {
         float h[8];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          if constexpr (EXP == 1) {  // timing experiment: no GELU
-            h[r] = acc1[2 * kp][tt][r] + bb[r];
-            h[4 + r] = acc1[2 * kp + 1][tt][r] + bb[16 + r];
-          } else {
-            h[r] = gelu_erf_fast(acc1[2 * kp][tt][r] + bb[r]);
-            h[4 + r] = gelu_erf_fast(acc1[2 * kp + 1][tt][r] + bb[16 + r]);
-          }
+          h[r] = gelu_erf_fast(acc1[2 * kp][tt][r] + bb[r]);
+          h[4 + r] = gelu_erf_fast(acc1[2 * kp + 1][tt][r] + bb[16 + r]);
         }
         bf16x8 hi, lo;
         pack8(h, hi, lo);
@@ -339,10 +332,7 @@ __global__ void __launch_bounds__(512) mlp_fused_kernel(MlpParams p) {
 template <int C, int TT, int NC>
 void launch_mlp_c(const MlpParams& p, hipStream_t s) {
   const unsigned grid = (unsigned)((p.M + 128 * TT - 1) / (128 * TT));
-  static const int exp = getenv("MOCR_MLP_EXP") ? atoi(getenv("MOCR_MLP_EXP")) : 0;
-  if (p.w1lo && p.w2lo && exp == 1)
-    mlp_fused_kernel<C, TT, NC, 3, 1><<<grid, 512, 0, s>>>(p);
-  else if (p.w1lo && p.w2lo)
+  if (p.w1lo && p.w2lo)
     mlp_fused_kernel<C, TT, NC, 3><<<grid, 512, 0, s>>>(p);
   else
     mlp_fused_kernel<C, TT, NC, 1><<<grid, 512, 0, s>>>(p);
@@ -356,6 +346,8 @@ void launch_mlp_fused(const MlpParams& p, hipStream_t s) {
   if (p.M <= 0) return;
   if ((p.w1lo == nullptr) != (p.w2lo == nullptr)) throw std::runtime_error("mlp: lo planes for both or neither");
   switch (p.C) {
+    // rows per wave 16 TT and hidden chunk NC measured best (TT = 1 at C = 96: 514 vs 420 us
+    // per s1 block; TT = 2 at C = 192 spills)
     case 96: launch_mlp_c<96, 2, 64>(p, s); break;
     case 192: launch_mlp_c<192, 1, 32>(p, s); break;
     default: throw std::runtime_error("mlp: fused MLP built for C = 96, 192");
