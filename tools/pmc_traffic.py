@@ -16,13 +16,15 @@ import json
 import sys
 
 
-def classes_in_order():
+def classes_in_order(mlp_fused=()):
+    """Encoder dispatch classes in launch order; stages in `mlp_fused` run norm2 + MLP as one
+    kernel (mlp.hip) instead of layernorm, fc1, fc2."""
     names = ["split(weights)", "split(kv-weights)", "stem"]
     depth = (2, 2, 6, 2)
     for s in range(4):
         for _ in range(depth[s]):
-            names += [f"s{s+1}.ln_partition", f"s{s+1}.qkv", f"s{s+1}.wattn", f"s{s+1}.proj",
-                      f"s{s+1}.layernorm", f"s{s+1}.fc1", f"s{s+1}.fc2"]
+            names += [f"s{s+1}.ln_partition", f"s{s+1}.qkv", f"s{s+1}.wattn", f"s{s+1}.proj"]
+            names += [f"s{s+1}.mlp"] if s + 1 in mlp_fused else [f"s{s+1}.layernorm", f"s{s+1}.fc1", f"s{s+1}.fc2"]
         if s < 3:
             names += [f"merge{s+1}.ln", f"merge{s+1}"]
     names += ["split(memory)", "memproj", "crosskv"]
@@ -34,7 +36,8 @@ def main(fetch_csv, write_csv, out):
     keep = lambda r: "mocr" in r["Kernel_Name"] and "fold_mm" not in r["Kernel_Name"]
     f = [r for r in csv.DictReader(open(fetch_csv)) if keep(r)]
     w = [r for r in csv.DictReader(open(write_csv)) if keep(r)]
-    names = classes_in_order()
+    fused = sorted({1 if "mlp_fused_kernel<96" in r["Kernel_Name"] else 2 for r in f if "mlp_fused" in r["Kernel_Name"]})
+    names = classes_in_order(fused)
     fp32 = len(f) == len(names) - 3  # fp32 mode has no bf16 split kernels
     if fp32:
         names = [n for n in names if not n.startswith("split")]
