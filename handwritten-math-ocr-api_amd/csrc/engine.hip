@@ -967,6 +967,9 @@ struct mocr_engine {
   // Encoder: norm2 + MLP fused for the stages mlp.hip is built for (bf16 modes);
   // MOCR_MLP_FUSED=0 selects the separate LayerNorm / fc1 / fc2 kernels (A/B).
   const bool mlp_fused = !(getenv("MOCR_MLP_FUSED") != nullptr && atoi(getenv("MOCR_MLP_FUSED")) == 0);
+  // ... and norm1 + qkv + window attention + proj (wattn.hip); MOCR_ATTN_FUSED=0 selects
+  // the partition LayerNorm / qkv GEMM / attention / proj GEMM kernels (A/B).
+  const bool attn_fused = !(getenv("MOCR_ATTN_FUSED") != nullptr && atoi(getenv("MOCR_ATTN_FUSED")) == 0);
   int attn_passes() const {
     return cfg.precision == MOCR_PRECISION_FP32 ? 0 : (cfg.precision == MOCR_PRECISION_BF16X3 ? 3 : 1);
   }
@@ -1039,6 +1042,7 @@ struct mocr_engine {
     static const char* ln1_n[] = {"s1.ln1", "s2.ln1", "s3.ln1", "s4.ln1"};
     static const char* ln2_n[] = {"s1.ln2", "s2.ln2", "s3.ln2", "s4.ln2"};
     static const char* mlp_n[] = {"s1.mlp", "s2.mlp", "s3.mlp", "s4.mlp"};
+    static const char* attn_n[] = {"s1.attn", "s2.attn", "s3.attn", "s4.attn"};
     static const char* mln_n[] = {"merge1.ln", "merge2.ln", "merge3.ln"};
     const bool b16 = bf16_mode();
     // GEMM A operands: fp32 buffers, or their bf16 planes
@@ -1054,16 +1058,37 @@ struct mocr_engine {
         const SwinBlockW& w = lay->blocks[bi];
         const WinGeom& wg = g.win[j & 1];
         const long wrows = (long)B * wg.nWin * kWinTok;
-        timed(ln1_n[s], 0, 8.0 * wrows * C,
-              [&] { launch_ln_partition(X, W(w.n1w), W(w.n1b), xw32, XWh, XWl, B, C, wg, stream); });
-        gemm(qkv_n[s], opXW, wop(w.qkvw), W(w.qkvb), QKV, nullptr, nullptr, (int)wrows, 3 * C, C, EPI_STORE, nullptr,
-             rows);
-        timed(att_n[s], 4.0 * rows * kWinTok * C, 4.0 * (double)rows * 4 * C, [&] {
-          launch_window_attention(QKV, relbias[bi], relmask[bi], att32, ATTh, ATTl, B, C, g.heads, wg, attn_passes(),
-                                  stream);
-        });
-        gemm(proj_n[s], opATT, wop(w.projw), W(w.projb), X, nullptr, nullptr, (int)wrows, C, C, EPI_WINRES, &wg,
-             rows);
+        if (b16 && attn_fused && swin_attn_fused_supported(C)) {
+          // norm1 + qkv + W-MSA + proj + residual in one kernel (wattn.hip)
+          SwinAttnParams ap{};
+          ap.X = X;
+          ap.ln_g = W(w.n1w);
+          ap.ln_b = W(w.n1b);
+          ap.wqkv = dwh + w.qkvw;
+          ap.wqkv_lo = dwl ? dwl + w.qkvw : nullptr;
+          ap.bqkv = W(w.qkvb);
+          ap.wproj = dwh + w.projw;
+          ap.wproj_lo = dwl ? dwl + w.projw : nullptr;
+          ap.bproj = W(w.projb);
+          ap.table = relmask[bi];
+          ap.B = B;
+          ap.C = C;
+          ap.heads = g.heads;
+          ap.wg = wg;
+          timed(attn_n[s], 8.0 * rows * C * C + 4.0 * rows * kWinTok * C, 8.0 * rows * C + (dwl ? 4.0 : 2.0) * 4.0 * C * C,
+                [&] { launch_swin_attn_fused(ap, stream); });
+        } else {
+          timed(ln1_n[s], 0, 8.0 * wrows * C,
+                [&] { launch_ln_partition(X, W(w.n1w), W(w.n1b), xw32, XWh, XWl, B, C, wg, stream); });
+          gemm(qkv_n[s], opXW, wop(w.qkvw), W(w.qkvb), QKV, nullptr, nullptr, (int)wrows, 3 * C, C, EPI_STORE,
+               nullptr, rows);
+          timed(att_n[s], 4.0 * rows * kWinTok * C, 4.0 * (double)rows * 4 * C, [&] {
+            launch_window_attention(QKV, relbias[bi], relmask[bi], att32, ATTh, ATTl, B, C, g.heads, wg,
+                                    attn_passes(), stream);
+          });
+          gemm(proj_n[s], opATT, wop(w.projw), W(w.projb), X, nullptr, nullptr, (int)wrows, C, C, EPI_WINRES, &wg,
+               rows);
+        }
         if (b16 && mlp_fused && mlp_fused_supported(C)) {
           // norm2 + fc1 + GELU + fc2 + residual in one kernel (mlp.hip)
           MlpParams mp{};

@@ -110,6 +110,22 @@ struct MlpParams {
 bool mlp_fused_supported(int C);
 void launch_mlp_fused(const MlpParams& p, hipStream_t s);
 
+// Fused norm1 + window qkv + W-MSA + proj + residual of one Swin block (wattn.hip),
+// bf16 / bf16x3 (lo planes present) for C = 96, 192 (head dim 32).
+struct SwinAttnParams {
+  float* X;                   // [B, H, W, C] fp32 residual stream, updated in place
+  const float *ln_g, *ln_b;   // norm1
+  const void *wqkv, *wqkv_lo; // [3C, C] bf16 hi / lo planes
+  const float* bqkv;          // [3C]
+  const void *wproj, *wproj_lo;  // [C, C]
+  const float* bproj;         // [C]
+  const float* table;         // [4 window types][heads][64 q][64 key] bias + mask (build_relmask)
+  int B, C, heads;
+  WinGeom wg;
+};
+bool swin_attn_fused_supported(int C);
+void launch_swin_attn_fused(const SwinAttnParams& p, hipStream_t s);
+
 // x -> bf16 hi (and lo) planes.
 void launch_split_bf16(const float* x, uint16_t* hi, uint16_t* lo, size_t n, hipStream_t s);
 

@@ -1,0 +1,468 @@
+// Fused attention half of a Swin block on bf16 / bf16x3 MFMA (torchvision
+// SwinTransformerBlock: x = x + proj(W-MSA(norm1(x)))), for one shifted window per
+// workgroup and one head per wave.  Unfused, a stage-1 block moves ~2.3 GB through HBM
+// for these four ops (the LN'd window partition as bf16 planes, QKV written and read
+// back in fp32, the attention output planes, the residual); fused, X is read once and
+// read-modify-written once per token.
+//
+//  A. norm1 of the window's 49 tokens (shift roll and zero padding applied on the
+//     gather, as ln_partition_kernel) into LDS as bf16 hi / lo planes, 64 rows
+//     (rows 49..63 and padded tokens are zero rows, F.pad after norm1);
+//  B. wave h: q^T, k^T = W_{q,k}[head h] . LN^T and v = LN . W_v[head h]^T over the
+//     C channels (W fragments straight from global, LN fragments from LDS).  The
+//     accumulators ARE the attention operands (no data movement):
+//       - K (A of S^T = K Q^T): lane (g, j) holds key j of a tile and dims
+//         {4g..4g+3} of k^T tile 0, {16+4g..} of tile 1: a permuted k order, the
+//         same for Q (B of S^T), so the contraction is unchanged;
+//       - V^T (A of O^T = V^T P^T): lane (g, j) holds dim j and keys 4g+r of the
+//         token tiles 2s, 2s+1 (swin.hip window_attention_mfma_kernel's key order);
+//  C. S^T, bias + mask table, softmax, O^T as in window_attention_mfma_kernel;
+//  D. O^T fragments (lane (g, j): token j, dims {4g+r, 16+4g+r} of head h) go to LDS
+//     as the B fragments of proj's k-step h; wave w computes out^T rows 32w .. 32w+31
+//     (A = W_proj rows, the same permuted k order), adds bias + residual and scatters
+//     to the window-reversed, un-rolled pixel (EPI_WINRES's mapping).
+#include "kernels.h"
+
+namespace mocr {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void pack8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) split2_bf16(v[2 * e], v[2 * e + 1], h[e], l[e]);
+  hi = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
+  lo = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
+}
+
+// c += a . b with a, b as bf16 hi (/ lo) planes: hi*hi (+ hi*lo + lo*hi for bf16x3)
+template <bool X3>
+__device__ __forceinline__ floatx4 mma(const bf16x8 (&a)[2], const bf16x8 (&b)[2], floatx4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
+  if constexpr (X3) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], c, 0, 0, 0);
+  }
+  return c;
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+// sum over aligned groups of L lanes (L = 8, 16): quad_perm xor 1, xor 2, then
+// row_half_mirror / row_mirror, which pair each lane with one of the other half's
+// lanes, all of which hold the same partial sum by then (== __shfl_xor by 4, 8)
+template <int L>
+__device__ __forceinline__ float row_sum(float s) {
+  static_assert(L == 8 || L == 16, "row_sum: 8 or 16 lanes");
+  s += dpp<0xB1>(s);
+  s += dpp<0x4E>(s);
+  s += dpp<0x141>(s);
+  if constexpr (L == 16) s += dpp<0x140>(s);
+  return s;
+}
+// x[lane ^ 16] and x[lane ^ 32] via v_permlane{16,32}_swap (VALU, no LDS queue).  The
+// swap exchanges halves between two registers, so both start as copies of x and their
+// sum / max is symmetric in the pair.  Inline asm: the builtin with one value for both
+// operands returned the same register twice (hardware-checked, tools/lane_ops_test.hip);
+// s_nop 1 covers the VALU-write -> permlane-read hazard.
+__device__ __forceinline__ void swap16(float& a, float& b) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ void swap32(float& a, float& b) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ float xmax16_32(float x) {
+  float a = x, b = x;
+  swap16(a, b);
+  x = fmaxf(a, b);
+  a = x;
+  b = x;
+  swap32(a, b);
+  return fmaxf(a, b);
+}
+__device__ __forceinline__ float xsum16_32(float x) {
+  float a = x, b = x;
+  swap16(a, b);
+  x = a + b;
+  a = x;
+  b = x;
+  swap32(a, b);
+  return a + b;
+}
+
+// 8 bf16 of row `row` (channels ch .. ch+7) of a [rows, C] plane pair
+template <bool X3>
+__device__ __forceinline__ void wfrag(const uint16_t* hi, const uint16_t* lo, int C, int row, int ch,
+                                      bf16x8 (&f)[2]) {
+  const size_t o = (size_t)row * C + ch;
+  f[0] = *reinterpret_cast<const bf16x8*>(hi + o);
+  if constexpr (X3) f[1] = *reinterpret_cast<const bf16x8*>(lo + o);
+}
+
+// channels {ch .. ch+3, ch+16 .. ch+19} of row `row` (proj's permuted k order)
+template <bool X3>
+__device__ __forceinline__ void wfrag_perm(const uint16_t* hi, const uint16_t* lo, int C, int row, int ch,
+                                           bf16x8 (&f)[2]) {
+  const size_t o = (size_t)row * C + ch;
+  const uint2 a = *reinterpret_cast<const uint2*>(hi + o);
+  const uint2 b = *reinterpret_cast<const uint2*>(hi + o + 16);
+  f[0] = __builtin_bit_cast(bf16x8, make_uint4(a.x, a.y, b.x, b.y));
+  if constexpr (X3) {
+    const uint2 c = *reinterpret_cast<const uint2*>(lo + o);
+    const uint2 d = *reinterpret_cast<const uint2*>(lo + o + 16);
+    f[1] = __builtin_bit_cast(bf16x8, make_uint4(c.x, c.y, d.x, d.y));
+  }
+}
+
+template <int C, int PASSES, int OCC>
+__global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC))) swin_attn_kernel(SwinAttnParams p) {
+  constexpr bool X3 = PASSES == 3;
+  constexpr int PL = X3 ? 2 : 1;
+  constexpr int HEADS = C / 32;  // = waves = k-steps of every GEMM here
+  constexpr int NT = 64 * HEADS;
+  constexpr int RC = C / 8;      // 16-B chunks per LN row
+  // chunk c of row r at c ^ s(r): conflict-free ds_read_b128 fragment reads (mlp.hip W1 image)
+  constexpr int SW = (RC % 16 == 0) ? 16 : ((RC % 8 == 0) ? 8 : 4);
+  constexpr int SH = SW == 16 ? 0 : 1;
+  constexpr int XB = 64 * C * 2;  // bytes per plane: the LN'd window, later proj's B fragments
+  constexpr int LPR = C / 12;     // lanes per row in the LayerNorm (12 floats each)
+  static_assert(RC % SW == 0 && 64 % LPR == 0, "layout");
+  __shared__ __attribute__((aligned(16))) char lds[PL * XB];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int h = tid >> 6;
+  const int j16 = lane & 15;
+  const int g = lane >> 4;
+  const WinGeom& wg = p.wg;
+  const int b = (int)(blockIdx.x / (unsigned)wg.nWin);
+  const int win = (int)(blockIdx.x - (unsigned)b * wg.nWin);
+  const int wy = win / wg.nWx;
+  const int wx = win - wy * wg.nWx;
+  // X row of window token tk, -1 for the padded tokens and slots 49..63
+  auto pixel = [&](int tk) -> long {
+    const int ty = tk / kWin;
+    int y = wy * kWin + ty + wg.sh;
+    int x = wx * kWin + (tk - ty * kWin) + wg.sw;
+    if (y >= wg.pH) y -= wg.pH;
+    if (x >= wg.pW) x -= wg.pW;
+    return (tk < kWinTok && y < wg.H && x < wg.W) ? (long)(b * wg.H + y) * wg.W + x : -1L;
+  };
+
+  // ---- A: norm1 into LDS (ln_group_kernel's lanes per row and summation order; the xor
+  // reductions as DPP moves, which add the same pairs; 1/C and rsqrt as multiplies)
+  {
+    constexpr int RPP = NT / LPR;              // rows per pass (24)
+    constexpr int NP = (64 + RPP - 1) / RPP;   // passes (3)
+    const int gi = lane % LPR;
+    const int c0 = gi * 12;
+    float v[NP][12];
+    long px[NP];
+#pragma unroll
+    for (int ps = 0; ps < NP; ++ps) {  // every load first
+      px[ps] = pixel(ps * RPP + tid / LPR);
+      const float* src = p.X + (size_t)(px[ps] < 0 ? 0 : px[ps]) * C + c0;  // clamped, masked below
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        const floatx4 t = *reinterpret_cast<const floatx4*>(src + 4 * e);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[ps][4 * e + k] = t[k];
+      }
+    }
+    floatx4 gg[3], bb[3];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      gg[e] = *reinterpret_cast<const floatx4*>(p.ln_g + c0 + 4 * e);
+      bb[e] = *reinterpret_cast<const floatx4*>(p.ln_b + c0 + 4 * e);
+    }
+#pragma unroll
+    for (int ps = 0; ps < NP; ++ps) {
+      const int r = ps * RPP + tid / LPR;
+      float s = 0.f;
+#pragma unroll
+      for (int e = 0; e < 12; ++e) s += v[ps][e];
+      s = row_sum<LPR>(s);
+      const float mean = s * (1.0f / C);
+      float q = 0.f;
+#pragma unroll
+      for (int e = 0; e < 12; ++e) {
+        const float d = v[ps][e] - mean;
+        q += d * d;
+      }
+      q = row_sum<LPR>(q);
+      const float rstd = rsqrtf(q * (1.0f / C) + 1e-5f);
+      const bool zero = px[ps] < 0;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        float y[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) y[k] = zero ? 0.f : (v[ps][4 * e + k] - mean) * rstd * gg[e][k] + bb[e][k];
+        uint32_t h0, l0, h1, l1;
+        split2_bf16(y[0], y[1], h0, l0);
+        split2_bf16(y[2], y[3], h1, l1);
+        const int c = c0 + 4 * e;
+        const int off = r * (2 * C) + (((c >> 3) ^ ((r >> SH) & (SW - 1))) << 4) + ((c >> 2) & 1) * 8;
+        if (ps * RPP + RPP <= 64 || r < 64) {
+          *reinterpret_cast<uint2*>(lds + off) = make_uint2(h0, h1);
+          if constexpr (X3) *reinterpret_cast<uint2*>(lds + XB + off) = make_uint2(l0, l1);
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- B: k^T, v, q^T of head h, one 8-tile GEMM at a time (each converted to its
+  // attention fragments at once, so only one set of accumulators is live)
+  const uint16_t* wqh = static_cast<const uint16_t*>(p.wqkv);
+  const uint16_t* wql = static_cast<const uint16_t*>(p.wqkv_lo);
+  const float* bq = p.bqkv;
+  // LN fragment (tokens 16t + j16, channels 32ks + 8g ..): B of the k^T / q^T GEMMs, A of v's
+  auto xfrag = [&](int ks, int t, bf16x8(&f)[2]) {
+    const int r = 16 * t + j16;
+    const int off = r * (2 * C) + (((4 * ks + g) ^ ((r >> SH) & (SW - 1))) << 4);
+    f[0] = *reinterpret_cast<const bf16x8*>(lds + off);
+    if constexpr (X3) f[1] = *reinterpret_cast<const bf16x8*>(lds + XB + off);
+  };
+  // acc[f][t] = W[row0 + 16f + j16, :] . LN^T (features x tokens)
+  auto gemm_t = [&](int row0, floatx4(&acc)[2][4]) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[f][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < HEADS; ++ks) {
+      bf16x8 w[2][2];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) wfrag<X3>(wqh, wql, C, row0 + 16 * f + j16, 32 * ks + 8 * g, w[f]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        bf16x8 xf[2];
+        xfrag(ks, t, xf);
+#pragma unroll
+        for (int f = 0; f < 2; ++f) acc[f][t] = mma<X3>(w[f], xf, acc[f][t]);
+      }
+    }
+  };
+  bf16x8 kf[4][2], vf[2][2][2], qf4[4][2];
+  __builtin_amdgcn_s_setprio(1);
+  {
+    floatx4 acc[2][4];
+    gemm_t(C + 32 * h, acc);
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      float x[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        x[r] = acc[0][kt][r] + bq[C + 32 * h + 4 * g + r];
+        x[4 + r] = acc[1][kt][r] + bq[C + 32 * h + 16 + 4 * g + r];
+      }
+      pack8(x, kf[kt][0], kf[kt][1]);
+    }
+  }
+  {
+    // v [tokens x dims]: A = LN rows, B = W_v rows
+    floatx4 acc[4][2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t][0] = acc[t][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < HEADS; ++ks) {
+      bf16x8 w[2][2];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) wfrag<X3>(wqh, wql, C, 2 * C + 32 * h + 16 * f + j16, 32 * ks + 8 * g, w[f]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        bf16x8 xf[2];
+        xfrag(ks, t, xf);
+#pragma unroll
+        for (int f = 0; f < 2; ++f) acc[t][f] = mma<X3>(xf, w[f], acc[t][f]);
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      const float bv = bq[2 * C + 32 * h + 16 * dt + j16];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float x[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          x[r] = acc[2 * s][dt][r] + bv;
+          x[4 + r] = acc[2 * s + 1][dt][r] + bv;
+        }
+        pack8(x, vf[dt][s][0], vf[dt][s][1]);
+      }
+    }
+  }
+  {
+    floatx4 acc[2][4];
+    gemm_t(32 * h, acc);
+    const float scale = 0.17677669529663687f;  // 32 ** -0.5
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      float x[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        x[r] = (acc[0][qt][r] + bq[32 * h + 4 * g + r]) * scale;
+        x[4 + r] = (acc[1][qt][r] + bq[32 * h + 16 + 4 * g + r]) * scale;
+      }
+      pack8(x, qf4[qt][0], qf4[qt][1]);
+    }
+  }
+  __builtin_amdgcn_s_setprio(0);
+  __syncthreads();  // every wave is done with the LN rows: the region takes proj's operands
+
+  // ---- C: attention per 16-query tile
+  int type = 0;
+  if (wg.sh + wg.sw > 0) type = 2 * (wy == wg.nWin / wg.nWx - 1) + (wx == wg.nWx - 1);
+  const float* tb = p.table + ((size_t)type * HEADS + h) * 64 * 64;
+  floatx4 bm[4];  // bias + mask of the current query tile
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt) bm[kt] = *reinterpret_cast<const floatx4*>(tb + j16 * 64 + 16 * kt + 4 * g);
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {
+    if (qt > 0) {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+        bm[kt] = *reinterpret_cast<const floatx4*>(tb + (16 * qt + j16) * 64 + 16 * kt + 4 * g);
+    }
+    floatx4 st[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) st[kt] = mma<X3>(kf[kt], qf4[qt], floatx4{0.f, 0.f, 0.f, 0.f});
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        st[kt][r] = st[kt][r] + bm[kt][r];
+        m = fmaxf(m, st[kt][r]);
+      }
+    }
+    m = xmax16_32(m);
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        st[kt][r] = __expf(st[kt][r] - m);
+        sum += st[kt][r];
+      }
+    sum = xsum16_32(sum);
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = st[2 * s + (j >> 2)][j & 3];
+      pack8(x, pf[s][0], pf[s][1]);
+    }
+    floatx4 o[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      o[dt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) o[dt] = mma<X3>(vf[dt][s], pf[s], o[dt]);
+    }
+    // softmax normalisation after P.V (per query = per lane column); proj's B fragment
+    // (token q, channels 32h + {4g+r, 16+4g+r}), lane-linear in LDS
+    const float inv = __builtin_amdgcn_rcpf(sum);
+    float x[8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      x[r] = o[0][r] * inv;
+      x[4 + r] = o[1][r] * inv;
+    }
+    bf16x8 ohl[2];
+    pack8(x, ohl[0], ohl[1]);
+    const int off = ((qt * HEADS + h) * 64 + lane) * 16;
+    *reinterpret_cast<bf16x8*>(lds + off) = ohl[0];
+    if constexpr (X3) *reinterpret_cast<bf16x8*>(lds + XB + off) = ohl[1];
+  }
+  __syncthreads();
+
+  // ---- D: out^T rows 32h .. 32h+31 = W_proj . O^T, + bias + residual
+  const uint16_t* wph = static_cast<const uint16_t*>(p.wproj);
+  const uint16_t* wpl = static_cast<const uint16_t*>(p.wproj_lo);
+  long pxo[4];
+  floatx4 xres[2][4];  // the residual rows, loaded before the GEMM
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    pxo[t] = pixel(16 * t + j16);
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+      xres[f][t] = *reinterpret_cast<const floatx4*>(p.X + (size_t)(pxo[t] < 0 ? 0 : pxo[t]) * C + 32 * h + 16 * f +
+                                                     4 * g);
+  }
+  floatx4 ap[2][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) ap[0][t] = ap[1][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int hh = 0; hh < HEADS; ++hh) {
+    bf16x8 wa[2][2];
+#pragma unroll
+    for (int f = 0; f < 2; ++f) wfrag_perm<X3>(wph, wpl, C, 32 * h + 16 * f + j16, 32 * hh + 4 * g, wa[f]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      bf16x8 of[2];
+      const int off = ((t * HEADS + hh) * 64 + lane) * 16;
+      of[0] = *reinterpret_cast<const bf16x8*>(lds + off);
+      if constexpr (X3) of[1] = *reinterpret_cast<const bf16x8*>(lds + XB + off);
+#pragma unroll
+      for (int f = 0; f < 2; ++f) ap[f][t] = mma<X3>(wa[f], of, ap[f][t]);
+    }
+  }
+  __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int ch = 32 * h + 16 * f + 4 * g;
+    const floatx4 bp = *reinterpret_cast<const floatx4*>(p.bproj + ch);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (pxo[t] < 0) continue;
+      floatx4 xv = xres[f][t];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xv[r] = xv[r] + (ap[f][t][r] + bp[r]);
+      *reinterpret_cast<floatx4*>(p.X + (size_t)pxo[t] * C + ch) = xv;
+    }
+  }
+}
+
+template <int C, int OCC>
+void launch_c(const SwinAttnParams& p, hipStream_t s) {
+  const unsigned grid = (unsigned)((long)p.B * p.wg.nWin);
+  if (p.wqkv_lo)
+    swin_attn_kernel<C, 3, OCC><<<grid, 2 * C, 0, s>>>(p);
+  else
+    swin_attn_kernel<C, 1, OCC><<<grid, 2 * C, 0, s>>>(p);
+}
+
+// waves per SIMD the register allocation targets: 3 at C = 96 (534 vs 651 us per s1
+// block, 19 dwords spilled), 2 at C = 192 (509 vs 649 us: 94 spilled at 3).
+// MOCR_ATTN_OCC=2|3 overrides both (A/B).
+int attn_occ(int C) {
+  static const int v = getenv("MOCR_ATTN_OCC") ? atoi(getenv("MOCR_ATTN_OCC")) : 0;
+  if (v == 2 || v == 3) return v;
+  return C == 96 ? 3 : 2;
+}
+
+}  // namespace
+
+bool swin_attn_fused_supported(int C) { return C == 96 || C == 192; }
+
+void launch_swin_attn_fused(const SwinAttnParams& p, hipStream_t s) {
+  if (p.B <= 0) return;
+  if ((p.wqkv_lo == nullptr) != (p.wproj_lo == nullptr))
+    throw std::runtime_error("swin_attn: lo planes for both or neither");
+  if (p.heads * 32 != p.C) throw std::runtime_error("swin_attn: head dim must be 32");
+  switch (p.C) {
+    case 96: attn_occ(96) == 2 ? launch_c<96, 2>(p, s) : launch_c<96, 3>(p, s); break;
+    case 192: attn_occ(192) == 2 ? launch_c<192, 2>(p, s) : launch_c<192, 3>(p, s); break;
+    default: throw std::runtime_error("swin_attn: fused attention built for C = 96, 192");
+  }
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace mocr

@@ -49,6 +49,27 @@ def test_encoder_stages_match_oracle(pkg, g384):
         assert e < 1e-4, f"features[{k}] rel err {e}"
 
 
+@pytest.mark.parametrize("env", [{}, {"MOCR_ATTN_FUSED": "0"}, {"MOCR_MLP_FUSED": "0", "MOCR_ATTN_FUSED": "0"}])
+def test_bf16x3_encoder_stages_match_oracle(pkg, golden, env, monkeypatch):
+    """bf16x3 encoder stage by stage: the fused stage-1/2 attention half (wattn.hip) and
+    MLP half (mlp.hip), and the unfused kernels they replace (env A/B switches, read at
+    engine creation), all within 1e-4 of the fp32 oracle.  384x384: the stage-1 map is
+    96x96, padded to 98 (zero tokens) and rolled by 3 on odd blocks."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = golden("g384_b2_pert")
+    m = g["meta"]
+    eng, w = make_engine(pkg, m, precision="bf16x3")
+    imgs = pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m["img_kind"])
+    _, stages = model_ref.encode(model_ref.build_model(w), torch.from_numpy(imgs), stages=True)
+    eng.set_images(imgs)
+    for k, ref in enumerate(stages):
+        got = eng.encode_until(k, tuple(ref.shape))
+        e = rel_err(got, ref.numpy())
+        assert e < 1e-4, f"features[{k}] rel err {e}"
+    eng.close()
+
+
 def test_memory_matches_golden(pkg, g384):
     g, eng, w, imgs = g384
     eng.encode(imgs)
