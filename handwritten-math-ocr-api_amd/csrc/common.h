@@ -62,6 +62,7 @@ struct DecodeState {
   int nfinished;    // rows that have produced EOS
   int last_finish;  // max over rows of the first-EOS step
   int batch;
+  int bad_rows;     // rows whose logits held no finite maximum (NaN / inf): MocrError on the host
 };
 
 // True when step t must not write anything (read late, after the loads are issued).

@@ -717,6 +717,10 @@ __global__ void __launch_bounds__(256) beam_select_kernel(BeamParams p) {
     int all_fin = 1;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
+      if (!(tf[k] >= 0 && tf[k] < K * V)) {  // no finite candidate (NaN logits): see dec_argmax_kernel
+        atomicAdd(&p.st->bad_rows, 1);
+        tf[k] = k * V;
+      }
       const int parent = tf[k] / V;
       const int pr = b * K + parent;
       const int pfin = p.fin[pr];
@@ -851,8 +855,17 @@ __global__ void __launch_bounds__(256) dec_argmax_kernel(DecodeState* st, int t,
 #pragma unroll
   for (int w = 1; w < 4; ++w) merge(best, bidx, sum, sv[w], si_[w], ss[w]);
   if (dec_skip(stop_batch ? st : nullptr, t)) return;
+  // A row without a finite maximum (NaN logits never win `v > best`) would leave bidx at
+  // INT_MAX and gather the next embedding ~2^31 rows out of bounds: clamp it to a valid
+  // id and count the row; the host turns the count into an error after the decode.
+  if (!(bidx >= 0 && bidx < V && isfinite(best) && sum > 0.f)) {
+    if (tid == 0) atomicAdd(&st->bad_rows, 1);
+    bidx = 0;
+    sum = 1.f;
+  }
   if (tid == 0) {
-    const int next = forced ? forced[(size_t)b * ld_ids + t + 1] : bidx;
+    int next = forced ? forced[(size_t)b * ld_ids + t + 1] : bidx;
+    next = min(max(next, 0), V - 1);
     ids[(size_t)b * ld_ids + t + 1] = bidx;
     feed[(size_t)b * ld_ids + t + 1] = next;
     logp[(size_t)b * (ld_ids - 1) + t] = logf(1.0f / sum + 1e-10f);

@@ -773,7 +773,7 @@ struct mocr_engine {
     st = dalloc<DecodeState>(1);
   }
 
-  // [type][h][64 q x 64 key] table of the bf16 attention kernels: bias[h][q][key] plus the
+  // [type][h][64 q][64 key] table of the bf16 attention kernel: bias[h][q][key] plus the
   // shifted-window mask (-100 across regions, torchvision shifted_window_attention) of
   // window type (last window row, last window column), -inf on the padded keys 49..63,
   // 0 on the padded query rows.  A window's region ids depend only on whether it is
@@ -797,9 +797,7 @@ struct mocr_engine {
                 if (rq != rk) v += -100.0f;
               }
             }
-            // fragment order (swin.hip window_attention_mfma_kernel): [qt][kt][lane][r]
-            const int lane = ((k & 15) >> 2) * 16 + (q & 15);
-            t[((((size_t)type * h + hh) * 4 + (q >> 4)) * 4 + (k >> 4)) * 256 + lane * 4 + (k & 3)] = v;
+            t[(((size_t)type * h + hh) * 64 + q) * 64 + k] = v;
           }
     }
     MOCR_HIP_CHECK(hipMemcpy(dst, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice));
@@ -1461,6 +1459,9 @@ struct mocr_engine {
     }
     MOCR_HIP_CHECK(hipMemcpyAsync(&hs, st, sizeof(hs), hipMemcpyDeviceToHost, stream));
     MOCR_HIP_CHECK(hipStreamSynchronize(stream));
+    if (hs.bad_rows)
+      throw std::runtime_error("decode: " + std::to_string(hs.bad_rows) +
+                               " row-steps had non-finite logits (NaN/inf in the encoder memory or weights)");
     return stop_batch && hs.done_step != 0x7fffffff ? hs.done_step + 1 : max_steps;
   }
   void decode_beam_out(int K, int max_steps, int stop_mode, int32_t* ids_out, float* scores_out, int32_t* beam_ids_out,
@@ -1508,6 +1509,9 @@ struct mocr_engine {
     }
     MOCR_HIP_CHECK(hipMemcpyAsync(&hs, st, sizeof(hs), hipMemcpyDeviceToHost, stream));
     MOCR_HIP_CHECK(hipStreamSynchronize(stream));
+    if (hs.bad_rows)
+      throw std::runtime_error("decode: " + std::to_string(hs.bad_rows) +
+                               " row-steps had non-finite logits (NaN/inf in the encoder memory or weights)");
     return stop_batch && hs.done_step != 0x7fffffff ? hs.done_step + 1 : max_steps;
   }
 

@@ -122,7 +122,6 @@ struct SwinAttnParams {
   const float* table;         // [4 window types][heads][64 q][64 key] bias + mask (build_relmask)
   int B, C, heads;
   WinGeom wg;
-  unsigned long long* stamps;  // phase timestamps (tools/wattn_bench.hip builds only); nullptr
 };
 bool swin_attn_fused_supported(int C);
 void launch_swin_attn_fused(const SwinAttnParams& p, hipStream_t s);

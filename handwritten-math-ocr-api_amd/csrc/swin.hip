@@ -387,10 +387,9 @@ __global__ void __launch_bounds__(256) window_attention_kernel(const float* __re
 //   O^T = V^T P^T with k = keys permuted so that the B operand of k-step s is exactly the
 //                 P^T accumulators of key tiles 2s, 2s+1 (lane keys 4(l/16) + r, r = 0..3):
 //                 A = V[keys 32s + {0,16} + 4(l/16) + r][d 16dt + l%16].
-// `table` = [type][head] fp32 fragments: relative-position bias + shift mask for the
-// window type (last window row / column), -inf on the padded keys 49..63, stored in the
-// order the S^T accumulators are read, [qt][kt][lane][r] for query 16 qt + lane % 16 and
-// key 16 kt + 4 (lane / 16) + r (one contiguous 1 KB per tile; engine.hip build_relmask).  PASSES = 3: hi*hi + hi*lo + lo*hi (bf16x3), 1: hi*hi.
+// `table` = [type][head][64 q][64 key] fp32: relative-position bias + shift mask for the
+// window type (last window row / column), -inf on the padded keys 49..63 (host-built,
+// engine.hip build_relmask).  PASSES = 3: hi*hi + hi*lo + lo*hi (bf16x3), 1: hi*hi.
 typedef __bf16 abf16x8 __attribute__((ext_vector_type(8)));
 typedef uint16_t au16x8 __attribute__((ext_vector_type(8)));
 
@@ -499,7 +498,7 @@ __global__ void __launch_bounds__(256) window_attention_mfma_kernel(const float*
     float m = -INFINITY;
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
-      const floatx4 b = *reinterpret_cast<const floatx4*>(tb + ((qt * 4 + kt) * 64 + lane) * 4);
+      const floatx4 b = *reinterpret_cast<const floatx4*>(tb + q * 64 + 16 * kt + 4 * g);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         st[kt][r] = st[kt][r] + b[r];

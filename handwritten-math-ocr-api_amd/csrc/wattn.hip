@@ -21,8 +21,6 @@
 //     as the B fragments of proj's k-step h; wave w computes out^T rows 32w .. 32w+31
 //     (A = W_proj rows, the same permuted k order), adds bias + residual and scatters
 //     to the window-reversed, un-rolled pixel (EPI_WINRES's mapping).
-#include <algorithm>
-
 #include "kernels.h"
 
 namespace mocr {
@@ -120,25 +118,8 @@ __device__ __forceinline__ void wfrag_perm(const uint16_t* hi, const uint16_t* l
   }
 }
 
-// s_memtime at phase boundaries of a workgroup's last window, one slot row per wave
-// (tools/wattn_bench.hip defines WATTN_STAMPS; the engine build has none)
-#ifdef WATTN_STAMPS
-#define STAMP(i)                                                                                \
-  do {                                                                                          \
-    if (p.stamps && lane == 0)                                                                  \
-      p.stamps[((size_t)blockIdx.x * HEADS + h) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-#else
-#define STAMP(i) \
-  do {           \
-  } while (0)
-#endif
-
-// Persistent: workgroup blockIdx.x takes windows blockIdx.x, + gridDim.x, ...  While
-// window i's projection runs, window i+1's X rows and first W fragments are loaded.
-template <int C, int PASSES, int OCC, bool PERSIST>
-__global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)))
-swin_attn_kernel(SwinAttnParams p, int nwin) {
+template <int C, int PASSES, int OCC>
+__global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC))) swin_attn_kernel(SwinAttnParams p) {
   constexpr bool X3 = PASSES == 3;
   constexpr int PL = X3 ? 2 : 1;
   constexpr int HEADS = C / 32;  // = waves = k-steps of every GEMM here
@@ -149,11 +130,6 @@ swin_attn_kernel(SwinAttnParams p, int nwin) {
   constexpr int SH = SW == 16 ? 0 : 1;
   constexpr int XB = 64 * C * 2;  // bytes per plane: the LN'd window, later proj's B fragments
   constexpr int LPR = C / 12;     // lanes per row in the LayerNorm (12 floats each)
-  constexpr int RPP = NT / LPR;   // LayerNorm rows per pass (24)
-  constexpr int NP = (64 + RPP - 1) / RPP;  // passes (3)
-  constexpr int NS = 3 * HEADS;   // phase B stages: (k^T, v, q^T) x k-steps
-  constexpr int WD = C == 96 ? 3 : 4;  // W fragments in flight (stages ahead)
-  constexpr int WDP = C == 96 ? 2 : 3;  // proj's W fragments in flight (k-steps ahead)
   static_assert(RC % SW == 0 && 64 % LPR == 0, "layout");
   __shared__ __attribute__((aligned(16))) char lds[PL * XB];
 
@@ -162,15 +138,13 @@ swin_attn_kernel(SwinAttnParams p, int nwin) {
   const int h = tid >> 6;
   const int j16 = lane & 15;
   const int g = lane >> 4;
-  const int gi = lane % LPR;  // LayerNorm: lane's 12 channels
-  const int c0 = gi * 12;
   const WinGeom& wg = p.wg;
-  // X row of token tk of window w, -1 for the padded tokens and slots 49..63
-  auto pixel = [&](int w, int tk) -> long {
-    const int b = w / wg.nWin;
-    const int wi = w - b * wg.nWin;
-    const int wy = wi / wg.nWx;
-    const int wx = wi - wy * wg.nWx;
+  const int b = (int)(blockIdx.x / (unsigned)wg.nWin);
+  const int win = (int)(blockIdx.x - (unsigned)b * wg.nWin);
+  const int wy = win / wg.nWx;
+  const int wx = win - wy * wg.nWx;
+  // X row of window token tk, -1 for the padded tokens and slots 49..63
+  auto pixel = [&](int tk) -> long {
     const int ty = tk / kWin;
     int y = wy * kWin + ty + wg.sh;
     int x = wx * kWin + (tk - ty * kWin) + wg.sw;
@@ -178,27 +152,20 @@ swin_attn_kernel(SwinAttnParams p, int nwin) {
     if (x >= wg.pW) x -= wg.pW;
     return (tk < kWinTok && y < wg.H && x < wg.W) ? (long)(b * wg.H + y) * wg.W + x : -1L;
   };
-  const uint16_t* wqh = static_cast<const uint16_t*>(p.wqkv);
-  const uint16_t* wql = static_cast<const uint16_t*>(p.wqkv_lo);
-  const uint16_t* wph = static_cast<const uint16_t*>(p.wproj);
-  const uint16_t* wpl = static_cast<const uint16_t*>(p.wproj_lo);
-  const float* bq = p.bqkv;
 
-  // the X rows phase A normalises next (clamped address, masked in phase A), and norm1's
-  // weight and bias (reloaded with them: loop-invariant registers would stay live)
-  float v[NP][12];
-  long px[NP];
-  floatx4 gg[3], bb[3];
-  auto xload = [&](int w) {
+  // ---- A: norm1 into LDS (ln_group_kernel's lanes per row and summation order; the xor
+  // reductions as DPP moves, which add the same pairs; 1/C and rsqrt as multiplies)
+  {
+    constexpr int RPP = NT / LPR;              // rows per pass (24)
+    constexpr int NP = (64 + RPP - 1) / RPP;   // passes (3)
+    const int gi = lane % LPR;
+    const int c0 = gi * 12;
+    float v[NP][12];
+    long px[NP];
 #pragma unroll
-    for (int e = 0; e < 3; ++e) {
-      gg[e] = *reinterpret_cast<const floatx4*>(p.ln_g + c0 + 4 * e);
-      bb[e] = *reinterpret_cast<const floatx4*>(p.ln_b + c0 + 4 * e);
-    }
-#pragma unroll
-    for (int ps = 0; ps < NP; ++ps) {
-      px[ps] = pixel(w, ps * RPP + tid / LPR);
-      const float* src = p.X + (size_t)(px[ps] < 0 ? 0 : px[ps]) * C + c0;
+    for (int ps = 0; ps < NP; ++ps) {  // every load first
+      px[ps] = pixel(ps * RPP + tid / LPR);
+      const float* src = p.X + (size_t)(px[ps] < 0 ? 0 : px[ps]) * C + c0;  // clamped, masked below
 #pragma unroll
       for (int e = 0; e < 3; ++e) {
         const floatx4 t = *reinterpret_cast<const floatx4*>(src + 4 * e);
@@ -206,42 +173,20 @@ swin_attn_kernel(SwinAttnParams p, int nwin) {
         for (int k = 0; k < 4; ++k) v[ps][4 * e + k] = t[k];
       }
     }
-  };
-  bf16x8 wb[WD][2][2];
-  auto wload = [&](int s) {  // stage s's W fragments (fragment-major copy: 1 KB per load)
+    floatx4 gg[3], bb[3];
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      const size_t o = ((size_t)((h * NS + s) * 2 + f) * 64 + lane) * 8;
-      wb[s % WD][f][0] = *reinterpret_cast<const bf16x8*>(wqh + o);
-      if constexpr (X3) wb[s % WD][f][1] = *reinterpret_cast<const bf16x8*>(wql + o);
+    for (int e = 0; e < 3; ++e) {
+      gg[e] = *reinterpret_cast<const floatx4*>(p.ln_g + c0 + 4 * e);
+      bb[e] = *reinterpret_cast<const floatx4*>(p.ln_b + c0 + 4 * e);
     }
-  };
-  // LN fragment (tokens 16t + j16, channels 32ks + 8g ..): B of the k^T / q^T GEMMs, A of v's
-  auto xfrag = [&](int ks, int t, bf16x8(&f)[2]) {
-    const int r = 16 * t + j16;
-    const int off = r * (2 * C) + (((4 * ks + g) ^ ((r >> SH) & (SW - 1))) << 4);
-    f[0] = *reinterpret_cast<const bf16x8*>(lds + off);
-    if constexpr (X3) f[1] = *reinterpret_cast<const bf16x8*>(lds + XB + off);
-  };
-
-  int w = blockIdx.x;
-  if (w >= nwin) return;  // whole workgroup
-#pragma unroll
-  for (int s = 0; s < WD; ++s) wload(s);
-  xload(w);
-
-  for (; w < nwin; w += gridDim.x) {
-    STAMP(0);
-    // ---- A: norm1 into LDS (ln_group_kernel's lanes per row and summation order; the
-    // xor reductions as DPP moves, which add the same pairs; 1/C and rsqrt as multiplies)
 #pragma unroll
     for (int ps = 0; ps < NP; ++ps) {
       const int r = ps * RPP + tid / LPR;
-      float sm = 0.f;
+      float s = 0.f;
 #pragma unroll
-      for (int e = 0; e < 12; ++e) sm += v[ps][e];
-      sm = row_sum<LPR>(sm);
-      const float mean = sm * (1.0f / C);
+      for (int e = 0; e < 12; ++e) s += v[ps][e];
+      s = row_sum<LPR>(s);
+      const float mean = s * (1.0f / C);
       float q = 0.f;
 #pragma unroll
       for (int e = 0; e < 12; ++e) {
@@ -267,297 +212,240 @@ swin_attn_kernel(SwinAttnParams p, int nwin) {
         }
       }
     }
-    STAMP(1);
-    __syncthreads();
-    STAMP(2);
+  }
+  __syncthreads();
 
-    // ---- B: k^T, v, q^T of head h, one 8-tile GEMM at a time (each converted to its
-    // attention fragments at once, so only one set of accumulators is live), the W
-    // fragments WD stages ahead through the (k^T, v, q^T) x k-step stages
-    bf16x8 kf[4][2], vf[2][2][2], qf4[4][2];
-    __builtin_amdgcn_s_setprio(1);
-    {
-      floatx4 acc[2][4];
-      bf16x8 xb[4][2];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) xfrag(0, t, xb[t]);
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const int m = s / HEADS;  // 0: k^T, 1: v, 2: q^T
-        const int ks = s - m * HEADS;
-        if (ks == 0) {
-#pragma unroll
-          for (int f = 0; f < 2; ++f)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) acc[f][t] = floatx4{0.f, 0.f, 0.f, 0.f};
-        }
-        bf16x8 wc[2][2];
-#pragma unroll
-        for (int f = 0; f < 2; ++f) {
-          wc[f][0] = wb[s % WD][f][0];
-          wc[f][1] = wb[s % WD][f][1];
-        }
-        bf16x8 xc[4][2];  // this stage's LN fragments (read one stage ahead)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          xc[t][0] = xb[t][0];
-          xc[t][1] = xb[t][1];
-        }
-        if (s + WD < NS) wload(s + WD);
-        if (s + 1 < NS) {
-#pragma unroll
-          for (int t = 0; t < 4; ++t) xfrag((s + 1) % HEADS, t, xb[t]);
-        }
-        __builtin_amdgcn_sched_barrier(0);  // keep the prefetches here (the scheduler sinks them to their use)
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int f = 0; f < 2; ++f)
-            acc[f][t] = m == 1 ? mma<X3>(xc[t], wc[f], acc[f][t]) : mma<X3>(wc[f], xc[t], acc[f][t]);
-        if (ks == HEADS - 1 && m == 0) {  // k^T: A fragments of S^T
-#pragma unroll
-          for (int kt = 0; kt < 4; ++kt) {
-            float x[8];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              x[r] = acc[0][kt][r] + bq[C + 32 * h + 4 * g + r];
-              x[4 + r] = acc[1][kt][r] + bq[C + 32 * h + 16 + 4 * g + r];
-            }
-            pack8(x, kf[kt][0], kf[kt][1]);
-          }
-        }
-        if (ks == HEADS - 1 && m == 1) {  // v [tokens x dims] (acc[dt][t]): A fragments of O^T
-#pragma unroll
-          for (int dt = 0; dt < 2; ++dt) {
-            const float bv = bq[2 * C + 32 * h + 16 * dt + j16];
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-              float x[8];
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                x[r] = acc[dt][2 * s2][r] + bv;
-                x[4 + r] = acc[dt][2 * s2 + 1][r] + bv;
-              }
-              pack8(x, vf[dt][s2][0], vf[dt][s2][1]);
-            }
-          }
-        }
-        if (ks == HEADS - 1 && m == 2) {  // q^T, scaled: B fragments of S^T
-          const float scale = 0.17677669529663687f;  // 32 ** -0.5
-#pragma unroll
-          for (int qt = 0; qt < 4; ++qt) {
-            float x[8];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              x[r] = (acc[0][qt][r] + bq[32 * h + 4 * g + r]) * scale;
-              x[4 + r] = (acc[1][qt][r] + bq[32 * h + 16 + 4 * g + r]) * scale;
-            }
-            pack8(x, qf4[qt][0], qf4[qt][1]);
-          }
-        }
-      }
-    }
-    __builtin_amdgcn_s_setprio(0);
-    // bias + mask of query tile 0 (each next tile's is loaded one tile ahead)
-    const float* tb;
-    {
-      const int wi = w % wg.nWin;
-      const int wy = wi / wg.nWx;
-      const int wx = wi - wy * wg.nWx;
-      const int type = (wg.sh + wg.sw > 0) ? 2 * (wy == wg.nWin / wg.nWx - 1) + (wx == wg.nWx - 1) : 0;
-      tb = p.table + ((size_t)type * HEADS + h) * 64 * 64;
-    }
-    floatx4 bm[4];
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt) bm[kt] = *reinterpret_cast<const floatx4*>(tb + j16 * 64 + 16 * kt + 4 * g);
-    STAMP(3);
-    __syncthreads();  // every wave is done with the LN rows: the region takes proj's operands
-    STAMP(4);
-
-    // ---- C: attention per 16-query tile
-#pragma unroll
-    for (int qt = 0; qt < 4; ++qt) {
-      floatx4 bmn[4];
-      if (qt < 3) {
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
-          bmn[kt] = *reinterpret_cast<const floatx4*>(tb + (16 * (qt + 1) + j16) * 64 + 16 * kt + 4 * g);
-      }
-      floatx4 st[4];
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) st[kt] = mma<X3>(kf[kt], qf4[qt], floatx4{0.f, 0.f, 0.f, 0.f});
-      float m = -INFINITY;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          st[kt][r] = st[kt][r] + bm[kt][r];
-          m = fmaxf(m, st[kt][r]);
-        }
-      }
-      m = xmax16_32(m);
-      float sum = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          st[kt][r] = __expf(st[kt][r] - m);
-          sum += st[kt][r];
-        }
-      sum = xsum16_32(sum);
-      bf16x8 pf[2][2];
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        float x[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) x[j] = st[2 * s2 + (j >> 2)][j & 3];
-        pack8(x, pf[s2][0], pf[s2][1]);
-      }
-      floatx4 o[2];
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        o[dt] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) o[dt] = mma<X3>(vf[dt][s2], pf[s2], o[dt]);
-      }
-      // softmax normalisation after P.V (per query = per lane column); proj's B fragment
-      // (token q, channels 32h + {4g+r, 16+4g+r}), lane-linear in LDS
-      const float inv = __builtin_amdgcn_rcpf(sum);
-      float x[8];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        x[r] = o[0][r] * inv;
-        x[4 + r] = o[1][r] * inv;
-      }
-      bf16x8 ohl[2];
-      pack8(x, ohl[0], ohl[1]);
-      const int off = ((qt * HEADS + h) * 64 + lane) * 16;
-      *reinterpret_cast<bf16x8*>(lds + off) = ohl[0];
-      if constexpr (X3) *reinterpret_cast<bf16x8*>(lds + XB + off) = ohl[1];
-      if (qt < 3) {
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt) bm[kt] = bmn[kt];
-      }
-    }
-    // proj's first WDP k-steps of W fragments ahead of the barrier
-    bf16x8 wpb[WDP][2][2];
-    auto wpload = [&](int hh) {
-#pragma unroll
-      for (int f = 0; f < 2; ++f) wfrag_perm<X3>(wph, wpl, C, 32 * h + 16 * f + j16, 32 * hh + 4 * g, wpb[hh % WDP][f]);
-    };
-#pragma unroll
-    for (int hh = 0; hh < WDP; ++hh) wpload(hh);
-    STAMP(5);
-    __syncthreads();
-    STAMP(6);
-
-    // ---- D: out^T rows 32h .. 32h+31 = W_proj . O^T, + bias + residual; the next
-    // window's X rows and first W stages are loaded meanwhile
-    if constexpr (PERSIST) {
-      // unconditional (the last window reloads itself): a conditional load would keep the
-      // consumed registers live across the whole loop
-      const int wnext = w + (int)gridDim.x < nwin ? w + (int)gridDim.x : w;
-      xload(wnext);
-    }
-    long pxo[4];
-    floatx4 xres[2][4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      pxo[t] = pixel(w, 16 * t + j16);
-#pragma unroll
-      for (int f = 0; f < 2; ++f)
-        xres[f][t] = *reinterpret_cast<const floatx4*>(p.X + (size_t)(pxo[t] < 0 ? 0 : pxo[t]) * C + 32 * h +
-                                                       16 * f + 4 * g);
-    }
-    floatx4 ap[2][4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) ap[0][t] = ap[1][t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int hh = 0; hh < HEADS; ++hh) {
-      bf16x8 wa[2][2];
-#pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        wa[f][0] = wpb[hh % WDP][f][0];
-        wa[f][1] = wpb[hh % WDP][f][1];
-      }
-      if (hh + WDP < HEADS) wpload(hh + WDP);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        bf16x8 of[2];
-        const int off = ((t * HEADS + hh) * 64 + lane) * 16;
-        of[0] = *reinterpret_cast<const bf16x8*>(lds + off);
-        if constexpr (X3) of[1] = *reinterpret_cast<const bf16x8*>(lds + XB + off);
-#pragma unroll
-        for (int f = 0; f < 2; ++f) ap[f][t] = mma<X3>(wa[f], of, ap[f][t]);
-      }
-    }
-    __builtin_amdgcn_s_setprio(0);
-#pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      const floatx4 bp = *reinterpret_cast<const floatx4*>(p.bproj + 32 * h + 16 * f + 4 * g);
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) xres[f][t][r] = xres[f][t][r] + (ap[f][t][r] + bp[r]);
-    }
-    if constexpr (PERSIST) {
-#pragma unroll
-      for (int s = 0; s < WD; ++s) wload(s);  // the next window's first W stages
-    }
+  // ---- B: k^T, v, q^T of head h, one 8-tile GEMM at a time (each converted to its
+  // attention fragments at once, so only one set of accumulators is live)
+  const uint16_t* wqh = static_cast<const uint16_t*>(p.wqkv);
+  const uint16_t* wql = static_cast<const uint16_t*>(p.wqkv_lo);
+  const float* bq = p.bqkv;
+  // LN fragment (tokens 16t + j16, channels 32ks + 8g ..): B of the k^T / q^T GEMMs, A of v's
+  auto xfrag = [&](int ks, int t, bf16x8(&f)[2]) {
+    const int r = 16 * t + j16;
+    const int off = r * (2 * C) + (((4 * ks + g) ^ ((r >> SH) & (SW - 1))) << 4);
+    f[0] = *reinterpret_cast<const bf16x8*>(lds + off);
+    if constexpr (X3) f[1] = *reinterpret_cast<const bf16x8*>(lds + XB + off);
+  };
+  // acc[f][t] = W[row0 + 16f + j16, :] . LN^T (features x tokens)
+  auto gemm_t = [&](int row0, floatx4(&acc)[2][4]) {
 #pragma unroll
     for (int f = 0; f < 2; ++f)
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-        if (pxo[t] >= 0) *reinterpret_cast<floatx4*>(p.X + (size_t)pxo[t] * C + 32 * h + 16 * f + 4 * g) = xres[f][t];
-    STAMP(7);
-    if constexpr (!PERSIST) break;
-    __syncthreads();  // proj's operands read: the region takes the next window's LN rows
+      for (int t = 0; t < 4; ++t) acc[f][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < HEADS; ++ks) {
+      bf16x8 w[2][2];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) wfrag<X3>(wqh, wql, C, row0 + 16 * f + j16, 32 * ks + 8 * g, w[f]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        bf16x8 xf[2];
+        xfrag(ks, t, xf);
+#pragma unroll
+        for (int f = 0; f < 2; ++f) acc[f][t] = mma<X3>(w[f], xf, acc[f][t]);
+      }
+    }
+  };
+  bf16x8 kf[4][2], vf[2][2][2], qf4[4][2];
+  __builtin_amdgcn_s_setprio(1);
+  {
+    floatx4 acc[2][4];
+    gemm_t(C + 32 * h, acc);
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      float x[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        x[r] = acc[0][kt][r] + bq[C + 32 * h + 4 * g + r];
+        x[4 + r] = acc[1][kt][r] + bq[C + 32 * h + 16 + 4 * g + r];
+      }
+      pack8(x, kf[kt][0], kf[kt][1]);
+    }
   }
-}
-
-// resident workgroups per CU x CUs (hipOccupancy...), capped by the window count
-template <typename K>
-int persistent_grid(K kernel, int threads, int nwin) {
-  static int cap = 0;
-  if (cap == 0) {
-    int dev = 0, per_cu = 0, cus = 0;
-    MOCR_HIP_CHECK(hipGetDevice(&dev));
-    MOCR_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    MOCR_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0));
-    cap = std::max(1, per_cu) * cus;
+  {
+    // v [tokens x dims]: A = LN rows, B = W_v rows
+    floatx4 acc[4][2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t][0] = acc[t][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < HEADS; ++ks) {
+      bf16x8 w[2][2];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) wfrag<X3>(wqh, wql, C, 2 * C + 32 * h + 16 * f + j16, 32 * ks + 8 * g, w[f]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        bf16x8 xf[2];
+        xfrag(ks, t, xf);
+#pragma unroll
+        for (int f = 0; f < 2; ++f) acc[t][f] = mma<X3>(xf, w[f], acc[t][f]);
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      const float bv = bq[2 * C + 32 * h + 16 * dt + j16];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float x[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          x[r] = acc[2 * s][dt][r] + bv;
+          x[4 + r] = acc[2 * s + 1][dt][r] + bv;
+        }
+        pack8(x, vf[dt][s][0], vf[dt][s][1]);
+      }
+    }
   }
-  return std::min(cap, nwin);
-}
+  {
+    floatx4 acc[2][4];
+    gemm_t(32 * h, acc);
+    const float scale = 0.17677669529663687f;  // 32 ** -0.5
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      float x[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        x[r] = (acc[0][qt][r] + bq[32 * h + 4 * g + r]) * scale;
+        x[4 + r] = (acc[1][qt][r] + bq[32 * h + 16 + 4 * g + r]) * scale;
+      }
+      pack8(x, qf4[qt][0], qf4[qt][1]);
+    }
+  }
+  __builtin_amdgcn_s_setprio(0);
+  __syncthreads();  // every wave is done with the LN rows: the region takes proj's operands
 
-template <int C, int PASSES, int OCC>
-void launch_cp(const SwinAttnParams& p, hipStream_t s) {
-  const int nwin = p.B * p.wg.nWin;
-  // MOCR_ATTN_PERSIST=1: persistent workgroups that prefetch the next window (A/B; with
-  // bf16x3 the extra live registers spill: 539 vs 430 us per s1 launch)
-  static const bool persist = getenv("MOCR_ATTN_PERSIST") && atoi(getenv("MOCR_ATTN_PERSIST")) == 1;
-  if (persist) {
-    auto k = swin_attn_kernel<C, PASSES, OCC, true>;
-    k<<<persistent_grid(k, 2 * C, nwin), 2 * C, 0, s>>>(p, nwin);
-  } else {
-    swin_attn_kernel<C, PASSES, OCC, false><<<nwin, 2 * C, 0, s>>>(p, nwin);
+  // ---- C: attention per 16-query tile
+  int type = 0;
+  if (wg.sh + wg.sw > 0) type = 2 * (wy == wg.nWin / wg.nWx - 1) + (wx == wg.nWx - 1);
+  const float* tb = p.table + ((size_t)type * HEADS + h) * 64 * 64;
+  floatx4 bm[4];  // bias + mask of the current query tile
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt) bm[kt] = *reinterpret_cast<const floatx4*>(tb + j16 * 64 + 16 * kt + 4 * g);
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {
+    if (qt > 0) {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+        bm[kt] = *reinterpret_cast<const floatx4*>(tb + (16 * qt + j16) * 64 + 16 * kt + 4 * g);
+    }
+    floatx4 st[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) st[kt] = mma<X3>(kf[kt], qf4[qt], floatx4{0.f, 0.f, 0.f, 0.f});
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        st[kt][r] = st[kt][r] + bm[kt][r];
+        m = fmaxf(m, st[kt][r]);
+      }
+    }
+    m = xmax16_32(m);
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        st[kt][r] = __expf(st[kt][r] - m);
+        sum += st[kt][r];
+      }
+    sum = xsum16_32(sum);
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = st[2 * s + (j >> 2)][j & 3];
+      pack8(x, pf[s][0], pf[s][1]);
+    }
+    floatx4 o[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      o[dt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) o[dt] = mma<X3>(vf[dt][s], pf[s], o[dt]);
+    }
+    // softmax normalisation after P.V (per query = per lane column); proj's B fragment
+    // (token q, channels 32h + {4g+r, 16+4g+r}), lane-linear in LDS
+    const float inv = __builtin_amdgcn_rcpf(sum);
+    float x[8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      x[r] = o[0][r] * inv;
+      x[4 + r] = o[1][r] * inv;
+    }
+    bf16x8 ohl[2];
+    pack8(x, ohl[0], ohl[1]);
+    const int off = ((qt * HEADS + h) * 64 + lane) * 16;
+    *reinterpret_cast<bf16x8*>(lds + off) = ohl[0];
+    if constexpr (X3) *reinterpret_cast<bf16x8*>(lds + XB + off) = ohl[1];
+  }
+  __syncthreads();
+
+  // ---- D: out^T rows 32h .. 32h+31 = W_proj . O^T, + bias + residual
+  const uint16_t* wph = static_cast<const uint16_t*>(p.wproj);
+  const uint16_t* wpl = static_cast<const uint16_t*>(p.wproj_lo);
+  long pxo[4];
+  floatx4 xres[2][4];  // the residual rows, loaded before the GEMM
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    pxo[t] = pixel(16 * t + j16);
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+      xres[f][t] = *reinterpret_cast<const floatx4*>(p.X + (size_t)(pxo[t] < 0 ? 0 : pxo[t]) * C + 32 * h + 16 * f +
+                                                     4 * g);
+  }
+  floatx4 ap[2][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) ap[0][t] = ap[1][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int hh = 0; hh < HEADS; ++hh) {
+    bf16x8 wa[2][2];
+#pragma unroll
+    for (int f = 0; f < 2; ++f) wfrag_perm<X3>(wph, wpl, C, 32 * h + 16 * f + j16, 32 * hh + 4 * g, wa[f]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      bf16x8 of[2];
+      const int off = ((t * HEADS + hh) * 64 + lane) * 16;
+      of[0] = *reinterpret_cast<const bf16x8*>(lds + off);
+      if constexpr (X3) of[1] = *reinterpret_cast<const bf16x8*>(lds + XB + off);
+#pragma unroll
+      for (int f = 0; f < 2; ++f) ap[f][t] = mma<X3>(wa[f], of, ap[f][t]);
+    }
+  }
+  __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int ch = 32 * h + 16 * f + 4 * g;
+    const floatx4 bp = *reinterpret_cast<const floatx4*>(p.bproj + ch);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (pxo[t] < 0) continue;
+      floatx4 xv = xres[f][t];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xv[r] = xv[r] + (ap[f][t][r] + bp[r]);
+      *reinterpret_cast<floatx4*>(p.X + (size_t)pxo[t] * C + ch) = xv;
+    }
   }
 }
 
 template <int C, int OCC>
 void launch_c(const SwinAttnParams& p, hipStream_t s) {
+  const unsigned grid = (unsigned)((long)p.B * p.wg.nWin);
   if (p.wqkv_lo)
-    launch_cp<C, 3, OCC>(p, s);
+    swin_attn_kernel<C, 3, OCC><<<grid, 2 * C, 0, s>>>(p);
   else
-    launch_cp<C, 1, OCC>(p, s);
+    swin_attn_kernel<C, 1, OCC><<<grid, 2 * C, 0, s>>>(p);
 }
 
-// waves per SIMD the register allocation targets (MOCR_ATTN_OCC=2|3 overrides, A/B)
+// waves per SIMD the register allocation targets: 3 at C = 96 (534 vs 651 us per s1
+// block, 19 dwords spilled), 2 at C = 192 (509 vs 649 us: 94 spilled at 3).
+// MOCR_ATTN_OCC=2|3 overrides both (A/B).
 int attn_occ(int C) {
   static const int v = getenv("MOCR_ATTN_OCC") ? atoi(getenv("MOCR_ATTN_OCC")) : 0;
   if (v == 2 || v == 3) return v;
-  return 2;
+  return C == 96 ? 3 : 2;
 }
 
 }  // namespace
