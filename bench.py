@@ -6,8 +6,9 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 A step = encode + 128-step greedy decode of one 64-image batch (images resident in HBM),
-then, with N > 1 ranks, an RCCL all-gather of the decoded token streams (image-parallel
-shards, no other collective).  Each GPU pipelines its steps through R engine replicas
+then, with N > 1 ranks, an RCCL all-gather of the decoded token streams inside
+libmathocr.so (``mocr_group_gather_ids``; image-parallel shards, no other collective;
+torch.distributed over gloo carries only the group id, barriers and the timing max).  Each GPU pipelines its steps through R engine replicas
 (``pipeline.ReplicaPool``), so one batch's latency-bound decode overlaps the next
 batch's encoder; every step still runs the whole path on its own 64 images.  Rank 0
 prints one JSON line; ``value`` = all images all ranks processed / max-over-ranks time.
@@ -29,8 +30,9 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "images/sec + p50 per-image latency, Swin-T+8L-dec greedy@128tok, 1/2/4/8 GPU"
-# dense peaks (MI355X_MICROARCH.md); bf16x3 issues 3 bf16 MFMAs per product
-PEAK = {"f32": 157.3, "bf16": 2500.0, "bf16x3": 2500.0 / 3}
+# dense peaks (MI355X_MICROARCH.md): MFMA TFLOP/s by operand type, HBM GB/s
+PEAK = {"f32": 157.3, "bf16": 2500.0, "bf16x3": 2500.0}
+HBM_PEAK_GBS = 8000.0
 DTYPE = {"fp32": "f32", "bf16x3": "bf16x3", "bf16": "bf16"}
 
 
@@ -47,7 +49,8 @@ def parse():
                     help="engine replicas pipelining batches per GPU (throughput plateaus at 4-6: tools/pipeline_probe.py)")
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
-    ap.add_argument("--cpu-sample", type=int, default=32, help="images in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=16,
+                    help="images per CPU-baseline throughput run (BASELINE.md §3; bounded to ~10-30 s in total)")
     ap.add_argument("--no-isolated", dest="isolated", action="store_false", default=True,
                     help="skip the single-replica latency / roofline pass")
     ap.add_argument("--arch", default="swin", choices=["swin", "res18trans"],
@@ -60,22 +63,49 @@ def parse():
     return a
 
 
+def cpu_threads():
+    """torch.set_num_threads(len(os.sched_getaffinity(0))), capped by
+    OMP_NUM_THREADS where the box sets it (the GPU box's CPU share is smaller than the
+    machine the affinity mask shows)."""
+    n = len(os.sched_getaffinity(0))
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return n
+
+
 def cpu_baseline(args, pkg):
     """The oracle restatement of the reference CPU path (src/inference.py: full-prefix
-    re-decode, fp32, torch CPU) on a bounded sample of the same workload."""
+    re-decode, fp32, torch CPU) on a bounded sample of the same workload:
+    one warm-up, then the median of 3 runs at B=1 (latency) and at B=cpu_sample
+    (throughput), same seeded images and weights as the GPU run."""
+    import platform
     from oracle import model_ref
-    threads = torch.get_num_threads()
+    threads = cpu_threads()
+    torch.set_num_threads(threads)
     w = pkg.synth.make_weights(1234, "init")
     model = model_ref.build_model(w)
     n = args.cpu_sample
     imgs = torch.from_numpy(pkg.synth.make_images(n, *args.image, seed0=1000))
     model_ref.greedy_decode(model, images=imgs[:1], max_steps=2, stop="none")  # warm-up
-    t0 = time.perf_counter()
-    model_ref.greedy_decode(model, images=imgs, max_steps=args.tokens, stop="none")
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "images/sec", "cores": threads, "kind": "port",
-            "sample": f"{n} images {args.image[0]}x{args.image[1]}, {args.tokens} greedy steps, "
-                      f"full-prefix re-decode as src/inference.py, fp32 torch CPU, {dt:.1f} s"}
+
+    def timed(batch):
+        t0 = time.perf_counter()
+        model_ref.greedy_decode(model, images=imgs[:batch], max_steps=args.tokens, stop="none")
+        return time.perf_counter() - t0
+
+    lat = statistics.median(timed(1) for _ in range(3))
+    thr = statistics.median(timed(n) for _ in range(3))
+    cpu = platform.processor() or platform.machine()
+    try:
+        cpu = next(ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    return {"value": n / thr, "unit": "images/sec", "cores": threads, "kind": "port",
+            "b1_latency_ms": lat * 1e3, "cpu": cpu,
+            "sample": f"median of 3 runs of {n} images (and of 1 image for b1_latency_ms), {args.image[0]}x"
+                      f"{args.image[1]}, {args.tokens} greedy steps, full-prefix re-decode as src/inference.py, "
+                      f"fp32 torch CPU, {threads} threads; {n}-image run {thr:.1f} s"}
 
 
 def pmc_traffic(precision, cls):
@@ -91,19 +121,41 @@ def pmc_traffic(precision, cls):
 
 def roofline(stats, dtype, precision):
     """Dominant encoder GEMM class by event-timed GPU time: algorithmic FLOP per launch /
-    average launch duration, against the dense MFMA peak of the arithmetic."""
+    average launch duration, against the dense bf16 MFMA peak (fp32 MFMA in fp32 mode).
+    bf16x3 issues three bf16 MFMAs per product (hi*hi + hi*lo + lo*hi), so the MFMA issue
+    rate is 3x the algorithmic rate: reported beside it as mfma_issue_frac."""
     gemms = {k: v for k, v in stats.items()
-             if v["flops"] > 0 and "attn" not in k and not k.endswith("stem") and k != "r.enc"}
+             if v["flops"] > 0 and "attn" not in k and not k.endswith("stem") and k != "r.enc"
+             and not k.startswith("decode")}
     name, d = max(gemms.items(), key=lambda kv: kv[1]["total_ms"])
     avg_ms = d["total_ms"] / d["launches"]
     flops = d["flops"] / d["launches"]
     achieved = flops / (avg_ms * 1e-3) / 1e12
     peak = PEAK[dtype]
-    return {"kernel": f"gemm_{'f32' if dtype == 'f32' else 'bf16'}[{dtype}] {name}", "bound": "mfma",
-            "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
-            "traffic": pmc_traffic(precision, name),
-            "avg_launch_ms": avg_ms, "flops_per_launch": flops,
-            "algorithmic_bytes_per_launch": d["bytes"] / d["launches"]}
+    out = {"kernel": f"gemm_{'f32' if dtype == 'f32' else 'bf16'}[{dtype}] {name}", "bound": "mfma",
+           "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+           "traffic": pmc_traffic(precision, name),
+           "avg_launch_ms": avg_ms, "flops_per_launch": flops,
+           "algorithmic_bytes_per_launch": d["bytes"] / d["launches"]}
+    if dtype == "bf16x3":
+        out["mfma_issue_frac"] = 3 * achieved / peak
+    return out
+
+
+def roofline_decode(stats, precision):
+    """The greedy decode step (42 graph-captured dependent kernels) against HBM: the
+    algorithmic bytes of a step (engine.hip decode_step_bytes: weights, cross-attention
+    K/V, self-attention K/V, logits; fp32 as built) / the HIP-event step time."""
+    d = stats.get("decode.greedy")
+    if not d or not d["launches"]:
+        return None
+    step_ms = d["total_ms"] / d["launches"]
+    byts = d["bytes"] / d["launches"]
+    achieved = byts / (step_ms * 1e-3) / 1e9
+    return {"kernel": "greedy decode step (8 layers x 5 folded kernels + logits + argmax)", "bound": "hbm",
+            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+            "traffic": pmc_traffic(precision, "decode.step"), "avg_step_ms": step_ms,
+            "algorithmic_bytes_per_step": byts, "tflops": d["flops"] / d["launches"] / (step_ms * 1e-3) / 1e12}
 
 
 def main():
@@ -112,10 +164,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = f"cuda:{local}"
+    pkg = importlib.import_module("handwritten-math-ocr-api_amd")
+    grp = None
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    pkg = importlib.import_module("handwritten-math-ocr-api_amd")
+        dist.init_process_group("gloo")  # host-side control only
+        grp = pkg.parallel.RcclGroup(world, rank, local)  # RCCL inside libmathocr.so
     H, W = args.image
     B, S, R = args.batch, args.tokens, args.replicas
     dtype = DTYPE[args.precision]
@@ -149,7 +203,8 @@ def main():
     def run(n):
         lat = []
         for ids, dt in pool.imap(step, range(n)):
-            pkg.parallel.gather_ids(ids, world)  # RCCL all-gather of the token streams, in step order
+            if grp:
+                grp.gather_ids(ids)  # RCCL all-gather of the token streams, in step order
             lat.append(dt)
         return lat
 
@@ -164,7 +219,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -199,6 +254,8 @@ def main():
 
     if rank != 0:
         pool.close()
+        if grp:
+            grp.close()
         if world > 1:
             dist.destroy_process_group()
         return
@@ -232,7 +289,11 @@ def main():
         out["p50_image_latency_unloaded_ms"] = iso["batch_latency_ms"]
         out["p50_image_latency_b1_ms"] = iso["b1_latency_ms"]
         out["roofline"] = roofline(iso["stats"], dtype, args.precision)
-        out["encoder_ms_per_batch_events"] = sum(v["total_ms"] for v in iso["stats"].values()) / 3
+        rd = roofline_decode(iso["stats"], args.precision)
+        if rd:
+            out["roofline_decode"] = rd
+        out["encoder_ms_per_batch_events"] = sum(v["total_ms"] for k, v in iso["stats"].items()
+                                                 if not k.startswith("decode")) / 3
         out["kernel_classes"] = {k: {"launches": v["launches"], "avg_ms": v["total_ms"] / v["launches"],
                                      "tflops": v["flops"] / v["total_ms"] * 1e-9 if v["total_ms"] else None}
                                  for k, v in sorted(iso["stats"].items())}
@@ -240,6 +301,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(args, pkg)
     pool.close()
     print(json.dumps(out))
+    if grp:
+        grp.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -4,5 +4,5 @@ PTD504/handwritten-math-ocr-api.
 The package directory name contains hyphens, so import it with
 ``importlib.import_module("handwritten-math-ocr-api_amd")``.
 """
-from . import config, im2latex, inference, parallel, pipeline, preprocess, synth, utils, weights  # noqa: F401
+from . import config, im2latex, inference, parallel, pipeline, predict, preprocess, synth, utils, weights  # noqa: F401
 from .engine import DecodeResult, Engine, MocrError, load_library  # noqa: F401

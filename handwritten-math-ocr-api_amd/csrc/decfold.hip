@@ -16,8 +16,6 @@
 // Loads are never predicated per element: out-of-range rows / keys read a clamped valid
 // address and are masked after the load (hipcc turns `c ? *p : 0` into a branch and a
 // full vmcnt(0) wait per element).
-#include <cstdlib>
-
 #include "kernels.h"
 
 namespace mocr {
@@ -376,12 +374,8 @@ void launch_foldgemm(const FoldGemmParams& p, hipStream_t s) {
   if (!p.A1 || !p.A2 || !p.Wy || !p.by || !p.y || !p.y_stats) throw std::runtime_error("foldgemm: null operand");
   if (p.B <= 0) return;
   const dim3 grid(kD / 16 + p.NZ / 16, (p.B + 15) / 16);
-  static const int nw = getenv("MOCR_FOLD_WAVES") ? atoi(getenv("MOCR_FOLD_WAVES")) : 4;
-#define MOCR_FG(K1, S1, S2)                                                     \
-  if (nw == 8)                                                                  \
-    foldgemm_kernel<K1, S1, S2, 8><<<grid, 512, 0, s>>>(p);                     \
-  else                                                                          \
-    foldgemm_kernel<K1, S1, S2, 4><<<grid, 256, 0, s>>>(p);
+  // 4 waves split K (8-wave workgroups measured no faster)
+#define MOCR_FG(K1, S1, S2) foldgemm_kernel<K1, S1, S2, 4><<<grid, 256, 0, s>>>(p);
   if (p.K1 == 256 && !s1 && !s2) {
     MOCR_FG(256, false, false)
   } else if (p.K1 == 256 && !s1 && s2) {

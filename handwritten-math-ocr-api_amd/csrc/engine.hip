@@ -230,6 +230,8 @@ void check_config(const mocr_config& c) {
   req(c.precision == MOCR_PRECISION_FP32 || c.precision == MOCR_PRECISION_BF16 ||
           c.precision == MOCR_PRECISION_BF16X3,
       "precision");
+  req((c.variant & ~(MOCR_VARIANT_UNFUSED_ATTN | MOCR_VARIANT_UNFUSED_MLP | MOCR_VARIANT_DEC_UNFOLDED)) == 0,
+      "variant: unknown MOCR_VARIANT_* flag");
   req(c.sos_id >= 0 && c.sos_id < c.vocab && c.eos_id >= 0 && c.eos_id < c.vocab, "special ids");
 }
 
@@ -735,7 +737,7 @@ struct mocr_engine {
         bslot[i] = dalloc<int32_t>(R * ld_ids);
       }
     }
-    if (fold_on) {
+    if (fold_greedy()) {
       const size_t ff = cfg.d_ff;
       const size_t per = 2 * d * d + 3 * d + ff * 2 * d + 3 * ff + 3 * d * (ff + d) + 9 * d;
       fold_buf = dalloc<float>(per * L);
@@ -846,7 +848,7 @@ struct mocr_engine {
       launch_split_bf16(kvw_all, kvwh, kvwl, (size_t)cfg.n_layers * 2 * d * d, stream);
       MOCR_HIP_CHECK(hipStreamSynchronize(stream));
     }
-    if (fold_on) fold_decoder();
+    if (fold_greedy()) fold_decoder();
     MOCR_HIP_CHECK(hipDeviceSynchronize());
     weights_loaded = true;
     encoded = false;
@@ -954,22 +956,14 @@ struct mocr_engine {
   };
   Operand wop(size_t off) const { return {dw + off, dwh ? dwh + off : nullptr, dwl ? dwl + off : nullptr}; }
   bool bf16_mode() const { return cfg.precision != MOCR_PRECISION_FP32; }
-  // Greedy decoder: separate head-projection rowgemms + attention kernels by default.  The
-  // fused projection+attention kernel (one workgroup per (row, head)) re-reads the head's
-  // weight slice per row (48 MB of L2 traffic per self-attention layer at B = 64) and
-  // measured slower (decode-only, 3 replicas: 2757 vs 3230 img/s); MOCR_DEC_FUSED=1
-  // selects it.  Beam search always uses it (slot-table keys, shared image memory).
-  const bool fused_attn = getenv("MOCR_DEC_FUSED") != nullptr && atoi(getenv("MOCR_DEC_FUSED")) != 0;
-  // Greedy decoder on the folded step (5 kernels per layer, kernels.h FoldGemmParams);
-  // MOCR_DEC_FOLD=0 selects the 8-kernel step (A/B).
-  const bool fold_on = !(getenv("MOCR_DEC_FOLD") != nullptr && atoi(getenv("MOCR_DEC_FOLD")) == 0);
-  bool fold_greedy() const { return fold_on && !fused_attn; }
-  // Encoder: norm2 + MLP fused for the stages mlp.hip is built for (bf16 modes);
-  // MOCR_MLP_FUSED=0 selects the separate LayerNorm / fc1 / fc2 kernels (A/B).
-  const bool mlp_fused = !(getenv("MOCR_MLP_FUSED") != nullptr && atoi(getenv("MOCR_MLP_FUSED")) == 0);
-  // ... and norm1 + qkv + window attention + proj (wattn.hip); MOCR_ATTN_FUSED=0 selects
-  // the partition LayerNorm / qkv GEMM / attention / proj GEMM kernels (A/B).
-  const bool attn_fused = !(getenv("MOCR_ATTN_FUSED") != nullptr && atoi(getenv("MOCR_ATTN_FUSED")) == 0);
+  // Kernel-path variants (include/mathocr.h MOCR_VARIANT_*): the production path fuses
+  // norm1 + qkv + W-MSA + proj (wattn.hip) and norm2 + MLP (mlp.hip) in the bf16 modes for
+  // the stages those kernels are built for, and runs greedy decoding on the folded step
+  // (kernels.h FoldGemmParams).  Beam search always uses the projection+attention kernel
+  // (slot-table keys, shared image memory).
+  bool attn_fused() const { return !(cfg.variant & MOCR_VARIANT_UNFUSED_ATTN); }
+  bool mlp_fused() const { return !(cfg.variant & MOCR_VARIANT_UNFUSED_MLP); }
+  bool fold_greedy() const { return !(cfg.variant & MOCR_VARIANT_DEC_UNFOLDED); }
   int attn_passes() const {
     return cfg.precision == MOCR_PRECISION_FP32 ? 0 : (cfg.precision == MOCR_PRECISION_BF16X3 ? 3 : 1);
   }
@@ -1058,7 +1052,7 @@ struct mocr_engine {
         const SwinBlockW& w = lay->blocks[bi];
         const WinGeom& wg = g.win[j & 1];
         const long wrows = (long)B * wg.nWin * kWinTok;
-        if (b16 && attn_fused && swin_attn_fused_supported(C)) {
+        if (b16 && attn_fused() && swin_attn_fused_supported(C)) {
           // norm1 + qkv + W-MSA + proj + residual in one kernel (wattn.hip)
           SwinAttnParams ap{};
           ap.X = X;
@@ -1089,7 +1083,7 @@ struct mocr_engine {
           gemm(proj_n[s], opATT, wop(w.projw), W(w.projb), X, nullptr, nullptr, (int)wrows, C, C, EPI_WINRES, &wg,
                rows);
         }
-        if (b16 && mlp_fused && mlp_fused_supported(C)) {
+        if (b16 && mlp_fused() && mlp_fused_supported(C)) {
           // norm2 + fc1 + GELU + fc2 + residual in one kernel (mlp.hip)
           MlpParams mp{};
           mp.X = X;
@@ -1163,7 +1157,7 @@ struct mocr_engine {
   // search: self-attention keys through `slots`, memory row = row / mem_div).
   void record_layers(int B, int t, const DecodeState* stp, const int32_t* slots, int mem_div) {
     const int d = cfg.d_model, L = cfg.n_layers;
-    const bool fused = fused_attn || slots != nullptr || mem_div != 1;
+    const bool fused = slots != nullptr || mem_div != 1;
     if (!fused && fold_greedy()) return record_layers_fold(B, t, stp);
     const size_t cache_layer = (size_t)max_rows * cfg.max_pos * d;
     const size_t kv_layer = (size_t)cfg.max_batch * M * 2 * d;
@@ -1448,6 +1442,11 @@ struct mocr_engine {
                       fold ? qpos : nullptr, fold ? dzqkv : nullptr);
     const int chunks = (max_steps + kDecodeChunk - 1) / kDecodeChunk;
     DecodeState hs{};
+    hipEvent_t t0 = nullptr;
+    if (timing) {
+      t0 = get_event();
+      MOCR_HIP_CHECK(hipEventRecord(t0, stream));
+    }
     for (int c = 0; c < chunks; ++c) {
       MOCR_HIP_CHECK(hipGraphLaunch(graph_for(B, c, max_steps, want_logits, forced_host != nullptr, stop_batch),
                                     stream));
@@ -1458,11 +1457,40 @@ struct mocr_engine {
       }
     }
     MOCR_HIP_CHECK(hipMemcpyAsync(&hs, st, sizeof(hs), hipMemcpyDeviceToHost, stream));
+    const int n = stop_batch && hs.done_step != 0x7fffffff ? hs.done_step + 1 : max_steps;
+    if (timing) {
+      // the whole graph-captured greedy decode as one record (launches = steps run)
+      TimingRec r{"decode.greedy", t0, get_event(), 0.0, 0.0};
+      MOCR_HIP_CHECK(hipEventRecord(r.e1, stream));
+      for (int t = 0; t < n; ++t) {
+        r.flops += decode_step_flops(B, t);
+        r.bytes += decode_step_bytes(B, t);
+      }
+      pending.push_back(r);
+      flush_timing();
+      stats["decode.greedy"].launches += n - 1;
+    }
     MOCR_HIP_CHECK(hipStreamSynchronize(stream));
     if (hs.bad_rows)
       throw std::runtime_error("decode: " + std::to_string(hs.bad_rows) +
                                " row-steps had non-finite logits (NaN/inf in the encoder memory or weights)");
-    return stop_batch && hs.done_step != 0x7fffffff ? hs.done_step + 1 : max_steps;
+    return n;
+  }
+
+  // Algorithmic work of greedy step t over B rows (SURVEY.md §8(d), fp32 as built): every
+  // decoder weight and fc_out once, the cross-attention K/V of all layers, the self-attention
+  // K/V of positions 0..t read and position t written, the logits written.  FLOP: the
+  // per-row projections 2*(6 d^2 + 2 d ff) per layer + 2 V d, attention 4 d (keys) per layer.
+  double decode_step_bytes(int B, int t) const {
+    const double d = cfg.d_model, ff = cfg.d_ff, L = cfg.n_layers, V = cfg.vocab;
+    const double weights = L * (6 * d * d + 2 * d * ff) + V * d;
+    const double cross = (double)B * M * 2 * d * L;
+    const double self_kv = (double)B * (t + 2) * 2 * d * L;
+    return 4.0 * (weights + cross + self_kv + (double)B * V);
+  }
+  double decode_step_flops(int B, int t) const {
+    const double d = cfg.d_model, ff = cfg.d_ff, L = cfg.n_layers, V = cfg.vocab;
+    return (double)B * (L * (2 * (6 * d * d + 2 * d * ff) + 4 * d * ((t + 1) + M)) + 2 * V * d);
   }
   void decode_beam_out(int K, int max_steps, int stop_mode, int32_t* ids_out, float* scores_out, int32_t* beam_ids_out,
                        int32_t* n_steps_out) {

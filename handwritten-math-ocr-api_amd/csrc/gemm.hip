@@ -244,38 +244,6 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int BK16 = 32;
-constexpr int LDS16 = BK16 + 8;  // 40 bf16 = 80 B per row
-
-__device__ __forceinline__ uint16_t bf16_rne(float f) {
-  uint32_t u = __float_as_uint(f);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
-__device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
-
-template <int EPI>
-__device__ __forceinline__ void epi_store16(const GemmParams& p, int row, int col, float v) {
-  if constexpr (EPI == EPI_RESADD || EPI == EPI_WINRES) {
-    epi_store<EPI>(p, row, col, v);  // fp32 residual stream
-  } else {
-    if (p.bias) v += p.bias[col];
-    if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
-    const size_t off = (size_t)row * p.ldc + col;
-    if (p.C) {
-      if (EPI == EPI_STORE && p.col_split) {
-        const int blk = col / p.col_split;
-        p.C[blk * p.split_stride + (size_t)row * p.col_split + (col - blk * p.col_split)] = v;
-      } else {
-        p.C[off] = v;
-      }
-    }
-    if (p.C16) {
-      const uint16_t hi = bf16_rne(v);
-      static_cast<uint16_t*>(p.C16)[off] = hi;
-      if (p.C16lo) static_cast<uint16_t*>(p.C16lo)[off] = bf16_rne(v - bf16_to_f32(hi));
-    }
-  }
-}
 
 // GELU for the bf16 / bf16x3 epilogues: erf by Abramowitz & Stegun 7.1.26 (one
 // reciprocal, one exp, 6 FMAs, no branches; |erf error| <= 1.5e-7, two orders below the
@@ -294,7 +262,7 @@ __device__ __forceinline__ float gelu_fast(float x) {
 }
 
 // Row-vector epilogue: 8 consecutive columns of one output row (col % 8 == 0), the same
-// arithmetic as epi_store/epi_store16 element by element, but 16/32-B loads and stores.
+// arithmetic as epi_store element by element, but 16/32-B loads and stores.
 template <int EPI>
 __device__ __forceinline__ void epi_vec8(const GemmParams& p, int row, int col, float (&v)[8]) {
   if (p.bias) {
@@ -383,133 +351,6 @@ __device__ __forceinline__ void epi_vec8(const GemmParams& p, int row, int col, 
         *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.C16lo) + off) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
     }
   }
-}
-
-template <int TM, int TN, int WGM, int WGN, int EPI, int PASSES>
-__global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_kernel(GemmParams p) {
-  constexpr int BM = 16 * TM * WGM;
-  constexpr int BN = 16 * TN * WGN;
-  constexpr int NT = 64 * WGM * WGN;
-  constexpr int PL = PASSES == 3 ? 2 : 1;  // planes per operand
-  constexpr int A_CHUNKS = BM * (BK16 / 8);  // 16-B chunks per plane
-  constexpr int W_CHUNKS = BN * (BK16 / 8);
-  constexpr int A_CH = (A_CHUNKS + NT - 1) / NT;  // per thread
-  constexpr int W_CH = (W_CHUNKS + NT - 1) / NT;
-
-  __shared__ uint16_t lds[PL * (BM + BN) * LDS16];
-  uint16_t* As[PL];
-  uint16_t* Ws[PL];
-#pragma unroll
-  for (int q = 0; q < PL; ++q) {
-    As[q] = lds + q * BM * LDS16;
-    Ws[q] = lds + PL * BM * LDS16 + q * BN * LDS16;
-  }
-  const uint16_t* Ag[2] = {static_cast<const uint16_t*>(p.A), static_cast<const uint16_t*>(p.A_lo)};
-  const uint16_t* Wg[2] = {static_cast<const uint16_t*>(p.W), static_cast<const uint16_t*>(p.W_lo)};
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave / WGN;
-  const int wn = wave % WGN;
-  int tx, ty;
-  tile_of(p.N / BN, tx, ty);
-  const int row0 = ty * BM;
-  const int col0 = tx * BN;
-
-  u16x8 ra[PL][A_CH];
-  u16x8 rw[PL][W_CH];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int q = 0; q < PL; ++q) {
-#pragma unroll
-      for (int i = 0; i < A_CH; ++i) {
-        const int idx = tid + i * NT;
-        const int r = idx >> 2;
-        const int c = (idx & 3) * 8;
-        const int gr = row0 + r;
-        ra[q][i] = (idx < A_CHUNKS && gr < p.M)
-                       ? *reinterpret_cast<const u16x8*>(Ag[q] + (size_t)gr * p.lda + k0 + c) : u16x8{};
-      }
-#pragma unroll
-      for (int i = 0; i < W_CH; ++i) {
-        const int idx = tid + i * NT;
-        const int r = idx >> 2;
-        const int c = (idx & 3) * 8;
-        rw[q][i] = idx < W_CHUNKS ? *reinterpret_cast<const u16x8*>(Wg[q] + (size_t)(col0 + r) * p.ldw + k0 + c)
-                                  : u16x8{};
-      }
-    }
-  };
-  auto sstore = [&]() {
-#pragma unroll
-    for (int q = 0; q < PL; ++q) {
-#pragma unroll
-      for (int i = 0; i < A_CH; ++i) {
-        const int idx = tid + i * NT;
-        if (idx < A_CHUNKS) *reinterpret_cast<u16x8*>(&As[q][(idx >> 2) * LDS16 + (idx & 3) * 8]) = ra[q][i];
-      }
-#pragma unroll
-      for (int i = 0; i < W_CH; ++i) {
-        const int idx = tid + i * NT;
-        if (idx < W_CHUNKS) *reinterpret_cast<u16x8*>(&Ws[q][(idx >> 2) * LDS16 + (idx & 3) * 8]) = rw[q][i];
-      }
-    }
-  };
-
-  floatx4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  gload(0);
-  sstore();
-  __syncthreads();
-  const int l16 = lane & 15;
-  const int kq = 8 * (lane >> 4);
-  for (int k0 = 0; k0 < p.K; k0 += BK16) {
-    const bool more = k0 + BK16 < p.K;
-    if (more) gload(k0 + BK16);
-    bf16x8 a[PL][TM], b[PL][TN];
-#pragma unroll
-    for (int q = 0; q < PL; ++q) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-        a[q][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u16x8*>(
-                                                 &As[q][(wm * 16 * TM + i * 16 + l16) * LDS16 + kq]));
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        b[q][j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u16x8*>(
-                                                 &Ws[q][(wn * 16 * TN + j * 16 + l16) * LDS16 + kq]));
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
-        if constexpr (PASSES == 3) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
-        }
-      }
-    __syncthreads();
-    if (more) {
-      sstore();
-      __syncthreads();
-    }
-  }
-
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = row0 + wm * 16 * TM + i * 16 + 4 * (lane >> 4) + r;
-        const int col = col0 + wn * 16 * TN + j * 16 + l16;
-        if (row < p.M) epi_store16<EPI>(p, row, col, acc[i][j][r]);
-      }
 }
 
 // ---------------------------------------------------------------- LDS-DMA ring version
@@ -718,11 +559,7 @@ void launch_tile16(const GemmParams& p, hipStream_t s) {
   constexpr int BN = 16 * TN * WGN;
   dim3 grid((p.N / BN) * ((p.M + BM - 1) / BM));
   dim3 block(64 * WGM * WGN);
-#define MOCR_G16(E)                                                                       \
-  if constexpr (RING > 0)                                                                 \
-    gemm_bf16_ring_kernel<TM, TN, WGM, WGN, E, PASSES, RING><<<grid, block, 0, s>>>(p);   \
-  else                                                                                    \
-    gemm_bf16_kernel<TM, TN, WGM, WGN, E, PASSES><<<grid, block, 0, s>>>(p);
+#define MOCR_G16(E) gemm_bf16_ring_kernel<TM, TN, WGM, WGN, E, PASSES, RING><<<grid, block, 0, s>>>(p);
   switch (p.epi) {
     case EPI_STORE: MOCR_G16(EPI_STORE); break;
     case EPI_GELU: MOCR_G16(EPI_GELU); break;
@@ -944,17 +781,14 @@ __global__ void __launch_bounds__(512) gemm_bf16_stag_kernel(GemmParams p) {
 }
 
 // Staggered 256 x 256 kernel: measured (B=64, 384²) faster than the ring kernels on bf16x3
-// GEMMs with K <= N and enough tiles (s3.fc1 225 -> 217 us, s4.fc1 163 -> 154), slower with
-// K > N or few tiles and in plain bf16.  MOCR_GEMM_STAG_MIN: minimum tiles (default 384;
-// set it to 1 to force the kernel wherever N % 256 == 0, as the bitwise A/B does).
+// GEMMs with K <= N and at least 384 tiles (s3.fc1 225 -> 217 us, s4.fc1 163 -> 154),
+// slower with K > N or fewer tiles and in plain bf16.
+constexpr long kBigMinTiles = 384;
 template <int PASSES>
 bool try_stag(const GemmParams& p, hipStream_t s) {
-  static const char* env = getenv("MOCR_GEMM_STAG_MIN");
-  static const long min_tiles = env ? atol(env) : 384;
-  if (min_tiles <= 0 || p.N % 256 != 0 || p.K % (PASSES == 3 ? 32 : 64) != 0) return false;
-  if (!env && (PASSES != 3 || p.K > p.N)) return false;
+  if (PASSES != 3 || p.K > p.N || p.N % 256 != 0 || p.K % 32 != 0) return false;
   const long tiles = (long)((p.M + 255) / 256) * (p.N / 256);
-  if (tiles < min_tiles) return false;
+  if (tiles < kBigMinTiles) return false;
   const dim3 grid((unsigned)tiles);
   switch (p.epi) {
     case EPI_STORE: gemm_bf16_stag_kernel<EPI_STORE, PASSES><<<grid, 512, 0, s>>>(p); break;
@@ -971,8 +805,7 @@ bool try_stag(const GemmParams& p, hipStream_t s) {
 // tiles, but one k-tile in flight at one block per CU: measured (B=64, 384²) faster on
 // bf16x3 GEMMs with K <= N (s1.fc1 435 -> 393 us, s2.qkv 212 -> 174, s2.fc1 276 -> 237,
 // s4.qkv 149 -> 136) and slower with K > N (s2.fc2 232 -> 257, s3.fc2 180 -> 191) and in
-// plain bf16.  Used for bf16x3 with K <= N and >= MOCR_GEMM_BIG_MIN tiles (default 384;
-// 0 disables).
+// plain bf16.  Used for bf16x3 with K <= N and >= kBigMinTiles tiles.
 template <int TN, int PASSES>
 void launch_big_tile(const GemmParams& p, hipStream_t s) {
   constexpr int BM = 256, BN = 64 * TN;
@@ -988,8 +821,8 @@ void launch_big_tile(const GemmParams& p, hipStream_t s) {
 
 template <int PASSES>
 bool try_big_tile(const GemmParams& p, hipStream_t s) {
-  static const long min_tiles = getenv("MOCR_GEMM_BIG_MIN") ? atol(getenv("MOCR_GEMM_BIG_MIN")) : 384;
-  if (min_tiles <= 0 || PASSES != 3 || p.K > p.N) return false;
+  constexpr long min_tiles = kBigMinTiles;
+  if (PASSES != 3 || p.K > p.N) return false;
   const long mt = (p.M + 255) / 256;
   if (p.N % 256 == 0 && mt * (p.N / 256) >= min_tiles) {
     launch_big_tile<4, PASSES>(p, s);
@@ -1003,40 +836,14 @@ bool try_big_tile(const GemmParams& p, hipStream_t s) {
   return true;
 }
 
-template <int TM, int TN, int WGM, int WGN, int PASSES, int NST>
-void launch_ring(const GemmParams& p, hipStream_t s) {
-  constexpr int BM = 16 * TM * WGM, BN = 16 * TN * WGN;
-  const dim3 grid((p.N / BN) * ((p.M + BM - 1) / BM));
-  const dim3 block(64 * WGM * WGN);
-  switch (p.epi) {
-    case EPI_STORE: gemm_bf16_ring_kernel<TM, TN, WGM, WGN, EPI_STORE, PASSES, NST><<<grid, block, 0, s>>>(p); break;
-    case EPI_GELU: gemm_bf16_ring_kernel<TM, TN, WGM, WGN, EPI_GELU, PASSES, NST><<<grid, block, 0, s>>>(p); break;
-    case EPI_RESADD: gemm_bf16_ring_kernel<TM, TN, WGM, WGN, EPI_RESADD, PASSES, NST><<<grid, block, 0, s>>>(p); break;
-    case EPI_WINRES: gemm_bf16_ring_kernel<TM, TN, WGM, WGN, EPI_WINRES, PASSES, NST><<<grid, block, 0, s>>>(p); break;
-    default: throw std::runtime_error("gemm_bf16: bad epilogue");
-  }
-}
-
 template <int PASSES>
 void launch_bf16_passes(const GemmParams& p, hipStream_t s) {
-  // MOCR_GEMM_RING = 0 (register staging) | 2 | 3 (LDS-DMA ring depth); A/B switch
-  static const int ring = getenv("MOCR_GEMM_RING") ? atoi(getenv("MOCR_GEMM_RING")) : 2;
-  if (ring == 2 && try_stag<PASSES>(p, s)) return;
-  if (ring == 2 && try_big_tile<PASSES>(p, s)) return;
+  if (try_stag<PASSES>(p, s)) return;
+  if (try_big_tile<PASSES>(p, s)) return;
   if (p.N % 128 == 0) {  // 128 x 128, waves of 64 x 64
-    if (ring == 3)
-      launch_tile16<4, 4, 2, 2, PASSES, 3>(p, s);
-    else if (ring == 2)
-      launch_tile16<4, 4, 2, 2, PASSES, 2>(p, s);
-    else
-      launch_tile16<4, 4, 2, 2, PASSES, 0>(p, s);
+    launch_tile16<4, 4, 2, 2, PASSES, 2>(p, s);
   } else if (p.N % 96 == 0) {  // 128 x 96, waves of 64 x 48
-    if (ring == 3)
-      launch_tile16<4, 3, 2, 2, PASSES, 3>(p, s);
-    else if (ring == 2)
-      launch_tile16<4, 3, 2, 2, PASSES, 2>(p, s);
-    else
-      launch_tile16<4, 3, 2, 2, PASSES, 0>(p, s);
+    launch_tile16<4, 3, 2, 2, PASSES, 2>(p, s);
   } else {
     throw std::runtime_error("gemm_bf16: N must be a multiple of 96 or 128");
   }

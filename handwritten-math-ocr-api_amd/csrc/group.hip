@@ -1,0 +1,141 @@
+// Image-parallel group of include/mathocr.h (BASELINE config 3):
+// one process per GPU, each rank encodes and decodes its own shard of the global batch
+// with no collective on the data path, then the decoded token streams are all-gathered
+// over RCCL (xGMI) into every rank's device memory.
+//
+// RCCL is opened at run time (dlopen of librccl.so.1, RTLD_LOCAL) so that libmathocr.so
+// loads without it and its symbols never interpose with the RCCL a host framework may
+// have loaded; only rccl.h's types are used at compile time.  The gather runs on the
+// group's own HIP stream and returns when the result is in place.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "../../include/mathocr.h"
+#include "kernels.h"
+
+static_assert(NCCL_UNIQUE_ID_BYTES == MOCR_GROUP_ID_BYTES, "RCCL unique id size");
+
+namespace {
+
+struct Rccl {
+  void* h = nullptr;
+  ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+template <typename F>
+void bind(void* h, F& fn, const char* name) {
+  fn = reinterpret_cast<F>(dlsym(h, name));
+  if (!fn) throw std::runtime_error(std::string("librccl: missing symbol ") + name);
+}
+
+const Rccl& rccl() {
+  static Rccl r = [] {
+    Rccl x;
+    x.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!x.h) x.h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!x.h) throw std::runtime_error(std::string("cannot load librccl.so.1: ") + dlerror());
+    bind(x.h, x.get_unique_id, "ncclGetUniqueId");
+    bind(x.h, x.comm_init_rank, "ncclCommInitRank");
+    bind(x.h, x.comm_destroy, "ncclCommDestroy");
+    bind(x.h, x.all_gather, "ncclAllGather");
+    bind(x.h, x.error_string, "ncclGetErrorString");
+    return x;
+  }();
+  return r;
+}
+
+void check(ncclResult_t rc, const char* what) {
+  if (rc != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + rccl().error_string(rc));
+}
+
+thread_local std::string g_group_error;
+
+int group_fail(const std::exception& ex) {
+  g_group_error = ex.what();
+  if (auto* he = dynamic_cast<const mocr::HipError*>(&ex)) return -1000 - (int)he->code;
+  return -1;
+}
+
+}  // namespace
+
+struct mocr_group {
+  ncclComm_t comm = nullptr;
+  int world = 0, rank = 0, device = 0;
+  hipStream_t stream = nullptr;
+};
+
+extern "C" {
+
+const char* mocr_group_last_error(void) { return g_group_error.c_str(); }
+
+int mocr_group_unique_id(uint8_t* id_out) {
+  try {
+    if (!id_out) throw std::runtime_error("null id_out");
+    ncclUniqueId id;
+    check(rccl().get_unique_id(&id), "ncclGetUniqueId");
+    std::memcpy(id_out, id.internal, MOCR_GROUP_ID_BYTES);
+    return 0;
+  } catch (const std::exception& ex) {
+    return group_fail(ex);
+  }
+}
+
+int mocr_group_create(const uint8_t* id, int world, int rank, int hip_device, mocr_group** out) {
+  mocr_group* g = nullptr;
+  try {
+    if (!id || !out) throw std::runtime_error("null argument");
+    if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("rank / world out of range");
+    ncclUniqueId uid;
+    std::memcpy(uid.internal, id, MOCR_GROUP_ID_BYTES);
+    g = new mocr_group();
+    g->world = world;
+    g->rank = rank;
+    g->device = hip_device;
+    MOCR_HIP_CHECK(hipSetDevice(hip_device));
+    MOCR_HIP_CHECK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+    check(rccl().comm_init_rank(&g->comm, world, uid, rank), "ncclCommInitRank");
+    *out = g;
+    return 0;
+  } catch (const std::exception& ex) {
+    if (g) {
+      if (g->stream) (void)hipStreamDestroy(g->stream);
+      delete g;
+    }
+    if (out) *out = nullptr;
+    return group_fail(ex);
+  }
+}
+
+int mocr_group_destroy(mocr_group* g) {
+  if (!g) return 0;
+  (void)hipSetDevice(g->device);
+  if (g->comm) (void)rccl().comm_destroy(g->comm);
+  if (g->stream) (void)hipStreamDestroy(g->stream);
+  delete g;
+  return 0;
+}
+
+int mocr_group_gather_ids(mocr_group* g, const int32_t* ids_dev, int rows, int width, int32_t* ids_all_dev) {
+  try {
+    if (!g || !ids_dev || !ids_all_dev) throw std::runtime_error("null argument");
+    if (rows < 0 || width < 1) throw std::runtime_error("rows / width out of range");
+    MOCR_HIP_CHECK(hipSetDevice(g->device));
+    check(rccl().all_gather(ids_dev, ids_all_dev, (size_t)rows * width, ncclInt32, g->comm, g->stream),
+          "ncclAllGather");
+    MOCR_HIP_CHECK(hipStreamSynchronize(g->stream));
+    return 0;
+  } catch (const std::exception& ex) {
+    return group_fail(ex);
+  }
+}
+
+}  // extern "C"

@@ -441,12 +441,6 @@ void launch_c(const SwinAttnParams& p, hipStream_t s) {
 
 // waves per SIMD the register allocation targets: 3 at C = 96 (534 vs 651 us per s1
 // block, 19 dwords spilled), 2 at C = 192 (509 vs 649 us: 94 spilled at 3).
-// MOCR_ATTN_OCC=2|3 overrides both (A/B).
-int attn_occ(int C) {
-  static const int v = getenv("MOCR_ATTN_OCC") ? atoi(getenv("MOCR_ATTN_OCC")) : 0;
-  if (v == 2 || v == 3) return v;
-  return C == 96 ? 3 : 2;
-}
 
 }  // namespace
 
@@ -458,8 +452,8 @@ void launch_swin_attn_fused(const SwinAttnParams& p, hipStream_t s) {
     throw std::runtime_error("swin_attn: lo planes for both or neither");
   if (p.heads * 32 != p.C) throw std::runtime_error("swin_attn: head dim must be 32");
   switch (p.C) {
-    case 96: attn_occ(96) == 2 ? launch_c<96, 2>(p, s) : launch_c<96, 3>(p, s); break;
-    case 192: attn_occ(192) == 2 ? launch_c<192, 2>(p, s) : launch_c<192, 3>(p, s); break;
+    case 96: launch_c<96, 3>(p, s); break;
+    case 192: launch_c<192, 2>(p, s); break;
     default: throw std::runtime_error("swin_attn: fused attention built for C = 96, 192");
   }
   MOCR_HIP_CHECK(hipGetLastError());

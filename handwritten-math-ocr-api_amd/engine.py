@@ -23,13 +23,15 @@ LIB_PATH = os.path.join(_HERE, "lib", "libmathocr.so")
 PRECISION = {"fp32": 0, "bf16": 1, "bf16x3": 2}
 STOP = {"batch": 0, "none": 1}
 ARCH = {"swin": 0, "res18trans": 1}
-ABI_VERSION = 3
+ABI_VERSION = 4
+# kernel-path variants (include/mathocr.h MOCR_VARIANT_*): 0 = production
+VARIANT = {"unfused_attn": 1, "unfused_mlp": 2, "dec_unfolded": 4}
 
 
 class MocrConfig(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "img_h", "img_w", "vocab", "d_model", "n_heads", "d_ff", "n_layers", "max_pos",
-        "sos_id", "eos_id", "pad_id", "max_batch", "precision", "max_beam", "arch")]
+        "sos_id", "eos_id", "pad_id", "max_batch", "precision", "max_beam", "arch", "variant")]
 
 
 class KernelStat(ctypes.Structure):
@@ -71,6 +73,11 @@ def load_library(path: str = LIB_PATH):
         "mocr_debug_encode_until": (I, [P, I, I, f32p, SZ]),
         "mocr_set_timing": (I, [P, I]),
         "mocr_get_timing": (I, [P, ctypes.POINTER(KernelStat), I]),
+        "mocr_group_unique_id": (I, [ctypes.c_char_p]),
+        "mocr_group_create": (I, [ctypes.c_char_p, I, I, I, ctypes.POINTER(P)]),
+        "mocr_group_destroy": (I, [P]),
+        "mocr_group_last_error": (ctypes.c_char_p, []),
+        "mocr_group_gather_ids": (I, [P, P, I, I, P]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -86,15 +93,19 @@ def exported_symbols():
     return ["mocr_abi_version", "mocr_weight_count", "mocr_memory_tokens", "mocr_create", "mocr_destroy",
             "mocr_last_error", "mocr_load_weights", "mocr_set_images", "mocr_set_images_device", "mocr_encode",
             "mocr_get_memory", "mocr_decode", "mocr_decode_device", "mocr_decode_beam", "mocr_debug_encode_until",
-            "mocr_set_timing", "mocr_get_timing", "mocr_set_encoder_pos"]
+            "mocr_set_timing", "mocr_get_timing", "mocr_set_encoder_pos", "mocr_group_unique_id", "mocr_group_create",
+            "mocr_group_destroy", "mocr_group_last_error", "mocr_group_gather_ids"]
 
 
 def make_config(img_hw=(96, 320), vocab=synth.VOCAB, max_batch=64, precision="fp32", n_layers=synth.N_LAYERS,
                 max_pos=synth.MAX_POS, sos=synth.SOS_ID, eos=synth.EOS_ID, pad=synth.PAD_ID, max_beam=0,
-                arch="swin") -> MocrConfig:
+                arch="swin", variant=()) -> MocrConfig:
+    flags = 0
+    for v in variant:
+        flags |= VARIANT[v]
     return MocrConfig(img_h=img_hw[0], img_w=img_hw[1], vocab=vocab, d_model=synth.D_MODEL, n_heads=synth.N_HEADS,
                       d_ff=synth.D_FF, n_layers=n_layers, max_pos=max_pos, sos_id=sos, eos_id=eos, pad_id=pad,
-                      max_batch=max_batch, precision=PRECISION[precision], max_beam=max_beam, arch=ARCH[arch])
+                      max_batch=max_batch, precision=PRECISION[precision], max_beam=max_beam, arch=ARCH[arch], variant=flags)
 
 
 def _f32p(a):
@@ -130,9 +141,12 @@ class Engine:
 
     def __init__(self, img_hw=(96, 320), vocab=synth.VOCAB, max_batch=64, precision="fp32", device=0,
                  n_layers=synth.N_LAYERS, max_pos=synth.MAX_POS, sos=synth.SOS_ID, eos=synth.EOS_ID,
-                 pad=synth.PAD_ID, max_beam=0, arch="swin"):
+                 pad=synth.PAD_ID, max_beam=0, arch="swin", variant=()):
+        """``variant``: names from ``VARIANT`` selecting the unfused kernel sequences
+        (parity tests); empty in production."""
         self.lib = load_library()
-        self.cfg = make_config(img_hw, vocab, max_batch, precision, n_layers, max_pos, sos, eos, pad, max_beam, arch)
+        self.cfg = make_config(img_hw, vocab, max_batch, precision, n_layers, max_pos, sos, eos, pad, max_beam, arch,
+                               tuple(variant))
         self.max_beam = max_beam
         self.arch = arch
         self.img_hw = tuple(img_hw)

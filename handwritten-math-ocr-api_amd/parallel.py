@@ -1,12 +1,18 @@
-"""Image-parallel sharding across GPUs.
+"""Image-parallel sharding across GPUs (BASELINE config 3).
 
-Images are independent through the encoder and the greedy decoder, so a global batch
-is split into contiguous per-rank shards, one process and one ``Engine`` per GPU,
-with no collective on the data path.  The only exchange is the final gather of the
-decoded token streams (``[B_local, S+1]`` int32 per rank) to every rank — RCCL over
-xGMI with the ``nccl`` backend and CUDA tensors, or gloo on CPU.
+Images are independent through the Swin encoder and the greedy decoder, so a global
+batch is split into contiguous per-rank shards, one process and one ``Engine`` per GPU,
+with no collective on the data path.  The only exchange is the final all-gather of the
+decoded token streams (``[B_local, S+1]`` int32 per rank): ``RcclGroup`` runs it inside
+libmathocr.so over RCCL (xGMI) on device memory (``mocr_group_*`` in include/mathocr.h).
+``torch.distributed`` carries only host-side control -- the group's 128-byte unique id,
+barriers, the max-over-ranks timing -- never token data.  ``gather_ids_host`` is the same
+exchange over a host process group (gloo), for the multi-process CPU tests of the shard
+logic.
 """
 from __future__ import annotations
+
+import ctypes
 
 
 def shard_bounds(n_total: int, world: int, rank: int):
@@ -18,18 +24,84 @@ def shard_bounds(n_total: int, world: int, rank: int):
     return start, start + base + (1 if rank < extra else 0)
 
 
-def gather_ids(ids_local, world: int, group=None):
-    """All-gather equal-shaped per-rank id tensors and concatenate them in rank order."""
+class RcclGroup:
+    """One rank of an image-parallel group on HIP device ``device`` (mocr_group_create).
+
+    ``id_bytes``: the 128-byte unique id rank 0 made with ``RcclGroup.unique_id()``; with
+    ``pg`` (a torch.distributed process group, e.g. gloo) and no id, rank 0 makes it and
+    broadcasts it over ``pg`` -- host bytes only.  Collective: every rank constructs it."""
+
+    def __init__(self, world: int, rank: int, device: int, id_bytes: bytes | None = None, pg=None):
+        from .engine import MocrError, load_library
+        self.lib = load_library()
+        self.world, self.rank, self.device = world, rank, device
+        if id_bytes is None:
+            if world == 1:
+                id_bytes = self.unique_id()
+            else:
+                import torch.distributed as dist
+                box = [self.unique_id() if rank == 0 else None]
+                dist.broadcast_object_list(box, src=0, group=pg)
+                id_bytes = box[0]
+        if len(id_bytes) != 128:
+            raise ValueError("unique id must be 128 bytes")
+        h = ctypes.c_void_p()
+        rc = self.lib.mocr_group_create(id_bytes, world, rank, device, ctypes.byref(h))
+        if rc != 0:
+            raise MocrError(f"mocr_group_create failed ({rc}): {self.lib.mocr_group_last_error().decode()}")
+        self._h = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        from .engine import MocrError, load_library
+        lib = load_library()
+        buf = ctypes.create_string_buffer(128)
+        rc = lib.mocr_group_unique_id(buf)
+        if rc != 0:
+            raise MocrError(f"mocr_group_unique_id failed ({rc}): {lib.mocr_group_last_error().decode()}")
+        return buf.raw
+
+    def gather_ids(self, ids_local, out=None):
+        """All-gather a [rows, width] int32 CUDA tensor from every rank into [world*rows,
+        width] (rank order), on the device; returns ``out``."""
+        import torch
+        from .engine import MocrError
+        if not ids_local.is_cuda or ids_local.dtype != torch.int32 or ids_local.dim() != 2:
+            raise ValueError("ids must be a 2-D int32 CUDA tensor")
+        ids_local = ids_local.contiguous()
+        rows, width = ids_local.shape
+        if out is None:
+            out = torch.empty((self.world * rows, width), dtype=torch.int32, device=ids_local.device)
+        if tuple(out.shape) != (self.world * rows, width) or not out.is_contiguous():
+            raise ValueError("out must be a contiguous [world*rows, width] int32 tensor")
+        rc = self.lib.mocr_group_gather_ids(self._h, ctypes.c_void_p(ids_local.data_ptr()), rows, width,
+                                            ctypes.c_void_p(out.data_ptr()))
+        if rc != 0:
+            raise MocrError(f"mocr_group_gather_ids failed ({rc}): {self.lib.mocr_group_last_error().decode()}")
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.mocr_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def gather_ids_host(ids_local, world: int, group=None):
+    """All-gather equal-shaped per-rank CPU id tensors over a host process group (gloo)
+    and concatenate them in rank order (multi-process CPU tests)."""
     import torch
     import torch.distributed as dist
 
     if world == 1:
         return ids_local
     if ids_local.is_cuda:
-        out = torch.empty((world * ids_local.shape[0],) + tuple(ids_local.shape[1:]), dtype=ids_local.dtype,
-                          device=ids_local.device)
-        dist.all_gather_into_tensor(out, ids_local.contiguous(), group=group)
-        return out
+        raise ValueError("device ids go through RcclGroup.gather_ids")
     parts = [torch.empty_like(ids_local) for _ in range(world)]
     dist.all_gather(parts, ids_local.contiguous(), group=group)
     return torch.cat(parts, 0)

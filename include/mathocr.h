@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MOCR_ABI_VERSION 3
+#define MOCR_ABI_VERSION 4
 
 /* Arithmetic of the engine. */
 enum {
@@ -58,6 +58,19 @@ enum {
                             /* whose attention runs across the batch (:61-62), memory = W/32 tokens;   */
                             /* its per-forward random positional table is an input                     */
                             /* (mocr_set_encoder_pos); convs run bf16x3 (bf16 with MOCR_PRECISION_BF16)  */
+};
+
+/* Kernel-path variants (mocr_config.variant).  0 is the production path; the others keep
+ * the unfused kernel sequences the fused kernels replaced selectable, so the parity tests
+ * can check fused against unfused on the same engine build (they are bit-for-bit different
+ * roundings of the same math, each held to the oracle's tolerance). */
+enum {
+  MOCR_VARIANT_DEFAULT = 0,
+  MOCR_VARIANT_UNFUSED_ATTN = 1, /* Swin stages 1-2: LN-partition, qkv GEMM, window attention, proj */
+                                 /* GEMM as separate kernels instead of wattn.hip's fused kernel     */
+  MOCR_VARIANT_UNFUSED_MLP = 2,  /* Swin stages 1-2: LN, fc1, fc2 instead of mlp.hip's fused kernel */
+  MOCR_VARIANT_DEC_UNFOLDED = 4  /* greedy decoder on the 8-kernel step (LayerNorms applied by their */
+                                 /* consumers) instead of the folded 5-kernel step (decfold.hip)     */
 };
 
 /* Greedy stopping rule (src/inference.py:23-25). */
@@ -79,6 +92,7 @@ typedef struct mocr_config {
   int32_t precision;     /* MOCR_PRECISION_*                                                       */
   int32_t max_beam;      /* 0: greedy only; K <= 8: decoder buffers for max_batch*K hypotheses      */
   int32_t arch;          /* MOCR_ARCH_*                                                            */
+  int32_t variant;       /* MOCR_VARIANT_* flags; 0 in production                                  */
 } mocr_config;
 
 typedef struct mocr_engine mocr_engine;
@@ -166,6 +180,34 @@ typedef struct mocr_kernel_stat {
 
 int mocr_set_timing(mocr_engine* eng, int enabled); /* also resets the counters */
 int mocr_get_timing(mocr_engine* eng, mocr_kernel_stat* out, int max_records);
+
+/* ---- Image-parallel group (BASELINE config 3) ----------------
+ * One process per GPU.  Each rank encodes and decodes its own contiguous shard of the
+ * global batch on its own engine (no collective on the data path); the decoded token
+ * streams are then all-gathered over RCCL (xGMI) into every rank's device memory.  The
+ * reference has no multi-GPU inference (src/test_model.py:38-40 wraps the model in a
+ * non-working nn.DataParallel); this replaces the survey's sketch
+ * mocr_group_create(n_dev, devs) / mocr_group_predict with one process per device.
+ *
+ * RCCL is loaded at run time (librccl.so.1).  Rank 0 makes the 128-byte unique id with
+ * mocr_group_unique_id and hands it to the other ranks over the caller's own channel
+ * (bench.py: the torch.distributed store); every rank then calls mocr_group_create
+ * collectively.  Errors: negative return, message in mocr_group_last_error(). */
+#define MOCR_GROUP_ID_BYTES 128
+typedef struct mocr_group mocr_group;
+
+int mocr_group_unique_id(uint8_t* id_out /* [MOCR_GROUP_ID_BYTES] */);
+int mocr_group_create(const uint8_t* id /* [MOCR_GROUP_ID_BYTES] */, int world, int rank, int hip_device,
+                      mocr_group** out);
+int mocr_group_destroy(mocr_group* g);
+const char* mocr_group_last_error(void);
+
+/* Collective: every rank passes its shard's ids [rows, width] int32 (device memory, e.g.
+ * the ids mocr_decode_device wrote; equal rows on every rank); ids_all_dev [world*rows,
+ * width] receives all shards in rank order.  Runs on the group's HIP stream and returns
+ * when the result is complete; the caller orders ids_dev's producer before the call
+ * (mocr_decode_device returns after its copy has completed). */
+int mocr_group_gather_ids(mocr_group* g, const int32_t* ids_dev, int rows, int width, int32_t* ids_all_dev);
 
 #ifdef __cplusplus
 }

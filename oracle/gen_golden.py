@@ -175,7 +175,7 @@ def run_reference(mode, *, seed, variant, eos_boost, B, H, W, img_seed, img_kind
 
 
 def make_res18_fixture(name, *, seed, variant, eos_boost, B, H, W, pos_seed, steps, stub, img_seed=1000,
-                       img_kind="uniform", n_logit_steps=8):
+                       img_kind="uniform", n_logit_steps=8, n_logit_rows=None):
     """ResNet18-trans (BASELINE config 5): oracle/res18_ref.py vs the reference's own
     src/model_res18trans.py + src/inference.py, batch-global stop."""
     pkg = _pkg()
@@ -201,7 +201,8 @@ def make_res18_fixture(name, *, seed, variant, eos_boost, B, H, W, pos_seed, ste
                 img_kind=img_kind, pos_seed=pos_seed, steps=steps, stop="batch", n_steps=int(ys.shape[1] - 1),
                 pinned_by="reference glue src/model_res18trans.py + src/inference.py (torchvision resnet18 restated)")
     np.savez_compressed(os.path.join(GOLDEN, name + ".npz"), meta=json.dumps(meta), ids=ys.numpy().astype(np.int32),
-                        logits=logits[:, :n_logit_steps].astype(np.float32), memory=mem.numpy().astype(np.float32),
+                        logits=logits[:n_logit_rows, :n_logit_steps].astype(np.float32),
+                        memory=mem.numpy().astype(np.float32),
                         margins=model_ref.top2_margins(torch.from_numpy(logits)).astype(np.float32),
                         strings=np.asarray(strings))
     print(f"{name}: B={B} {H}x{W} steps={ys.shape[1] - 1} min-margin={model_ref.top2_margins(torch.from_numpy(logits)).min():.2e}")
@@ -245,6 +246,25 @@ def make_batch_fixture(name, *, seed, variant, eos_boost, B, H, W, img_seed=1000
     print(f"{name}: ids {tuple(ys.shape)} min-margin {margins.min():.2e} glue={'ok' if glue else '-'}")
 
 
+def make_beam_fixture(name, *, seed, variant, B, H, W, K, steps, max_pos, img_seed=1000, img_kind="uniform"):
+    """Beam search (BASELINE config 4 shape: 384x384, K = 4, 256 steps) on rows of the
+    bench batch.  The reference has no beam search, so the specification is
+    oracle/model_ref.py beam_search (parity unpinned by the reference); rows are
+    independent, so these B rows stand for the same rows of a larger batch."""
+    pkg = _pkg()
+    from oracle import model_ref
+    w = pkg.synth.make_weights(seed, variant, max_pos=max_pos)
+    imgs = pkg.synth.make_images(B, H, W, img_seed, img_kind)
+    model = model_ref.build_model(w)
+    mem = model_ref.encode(model, torch.from_numpy(imgs))
+    seqs, scores, n = model_ref.beam_search(model, memory=mem, beam=K, max_steps=steps, stop="none")
+    meta = dict(seed=seed, variant=variant, B=B, H=H, W=W, K=K, steps=steps, max_pos=max_pos, img_seed=img_seed,
+                img_kind=img_kind, stop="none", pinned_by="oracle/model_ref.py beam_search (no reference beam search)")
+    np.savez_compressed(os.path.join(GOLDEN, name + ".npz"), meta=json.dumps(meta),
+                        seqs=seqs.numpy().astype(np.int32), scores=scores.numpy().astype(np.float32))
+    print(f"{name}: seqs {tuple(seqs.shape)} scores[0]={scores[0].tolist()}")
+
+
 def make_serving_fixture(name, *, seed, variant, eos_boost, H, W, img_seed, img_kind, stub):
     pkg = _pkg()
     from oracle import model_ref
@@ -276,6 +296,17 @@ def main(only=None):
         make_res18_fixture("r96x320_b4_eos", seed=41, variant="perturbed", eos_boost=EOS_BOOST_R18, B=4, H=96,
                            W=320, img_kind="ink", pos_seed=6, steps=150, stub=stub)
     if only == "res18":
+        return
+    if only == "bench":
+        # BASELINE configs at full size, on the bench's own inputs (bench.py: weights seed 1234 "init",
+        # images PCG64 1000+i, 384x384): config 2 (Swin, B=64, greedy 128 steps), config 5
+        # (ResNet18-trans, B=64, pos table seed 5), config 4 (beam 4, 256 steps: rows 0-1).
+        make_batch_fixture("g384_b64_bench", seed=1234, variant="init", eos_boost=0.0, B=64, H=384, W=384,
+                           steps=128, stop="batch", n_logit_steps=4, stub=stub)
+        make_res18_fixture("r384_b64_bench", seed=1234, variant="init", eos_boost=0.0, B=64, H=384, W=384,
+                           pos_seed=5, steps=128, stub=stub, n_logit_steps=4, n_logit_rows=2)
+        make_beam_fixture("b384_k4_bench", seed=1234, variant="init", B=2, H=384, W=384, K=4, steps=256,
+                          max_pos=260)
         return
     # 384x384, perturbed weights, 128 fixed steps (BASELINE config shape; ids checked via glue with EOS unreachable).
     make_batch_fixture("g384_b2_pert", seed=11, variant="perturbed", eos_boost=0.0, B=2, H=384, W=384,

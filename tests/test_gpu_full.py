@@ -1,0 +1,117 @@
+"""GPU: the BASELINE configs at full size, on the bench's own inputs (bench.py: weights
+seed 1234 with the reference's init distributions, images PCG64 seeds 1000+i, 384x384,
+bf16x3 -- the bench precision).  Fixtures: ``python -m oracle.gen_golden bench``.
+
+* config 2 -- Swin-T + 8-layer decoder, B=64, greedy 128 steps (fixture pinned by the
+  reference's own ``src/inference.py`` glue on the same 64 images);
+* config 5 -- ResNet18-trans, B=64, greedy 128 steps (the encoder attends across the
+  batch, so the whole batch is the unit; pinned by ``src/model_res18trans.py`` glue);
+* config 4 -- beam 4, 256 steps, B=32 (rows 0-1 against the beam specification of
+  ``oracle/model_ref.py``; the reference has no beam search).
+
+Token ids are compared exactly.  Over 64 rows x 128 steps a few steps have top-2 logit
+margins below what fp32 rounding of a different summation order can move (the fixture
+stores every step's margin; one ResNet step is an exact fp32 tie), so a row is compared
+in full when none of its steps is a near-tie, and up to and including its first
+near-tie step otherwise; teacher-forced decoding then checks every step's argmax of
+every row whose margin is above the tie threshold.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+LOGIT_TOL = 1e-3
+
+
+def rel_err(a, b):
+    return float(np.abs(a - b).max() / (np.abs(b).max() + 1e-12))
+
+
+def check_ids(got, ref, margins, tie):
+    """Exact ids; a row with a near-tie step (margin < tie) is compared up to that step."""
+    assert got.shape == ref.shape
+    n_full = 0
+    for r in range(ref.shape[0]):
+        near = np.flatnonzero(margins[r] < tie)
+        end = ref.shape[1] if near.size == 0 else int(near[0]) + 2  # column t+1 is step t's token
+        np.testing.assert_array_equal(got[r, :end], ref[r, :end], err_msg=f"row {r} (compared to column {end})")
+        n_full += near.size == 0
+    return n_full
+
+
+def check_teacher_forced(eng, ref_ids, margins, tie, ref_logits):
+    S = ref_ids.shape[1] - 1
+    tf = eng.decode(max_steps=S, stop="none", forced=ref_ids, want_logits=True)
+    am = tf.logits.argmax(-1)
+    ok = margins >= tie
+    assert ok.mean() > 0.99
+    np.testing.assert_array_equal(am[ok], ref_ids[:, 1:][ok])
+    r, n = ref_logits.shape[:2]
+    err = float(np.abs(tf.logits[:r, :n] - ref_logits).max())
+    assert err < LOGIT_TOL, err
+
+
+def test_config2_swin_b64_greedy128(pkg, golden):
+    g = golden("g384_b64_bench")
+    m = g["meta"]
+    assert (m["B"], m["H"], m["W"], m["steps"], m["seed"], m["variant"]) == (64, 384, 384, 128, 1234, "init")
+    eng = pkg.Engine(img_hw=(384, 384), max_batch=64, precision="bf16x3")
+    eng.load_weights(pkg.synth.make_weights(1234, "init"))
+    eng.encode(pkg.synth.make_images(64, 384, 384, seed0=1000))
+    mem = eng.memory()
+    assert rel_err(mem[:2], g["memory"]) < 1e-4
+    res = eng.decode(max_steps=128, stop="batch")
+    assert res.n_steps == g["ids"].shape[1] - 1
+    n_full = check_ids(res.ids, g["ids"], g["margins"], tie=1e-4)
+    assert n_full >= 60, n_full
+    check_teacher_forced(eng, g["ids"], g["margins"], 1e-4, g["logits"])
+    # determinism at full size, and the bench's no-stop decode gives the same tokens
+    again = eng.decode(max_steps=128, stop="none")
+    np.testing.assert_array_equal(again.ids, res.ids)
+    eng.close()
+
+
+def test_config5_res18trans_b64_greedy128(pkg, golden):
+    g = golden("r384_b64_bench")
+    m = g["meta"]
+    assert (m["B"], m["H"], m["W"], m["steps"], m["pos_seed"]) == (64, 384, 384, 128, 5)
+    eng = pkg.Engine(img_hw=(384, 384), max_batch=64, precision="bf16x3", arch="res18trans")
+    eng.load_weights(pkg.synth.make_weights(1234, "init", arch="res18trans"))
+    eng.set_encoder_pos(pkg.synth.make_pos_table(5, eng.memory_tokens))
+    eng.encode(pkg.synth.make_images(64, 384, 384, seed0=1000))
+    assert rel_err(eng.memory(), g["memory"]) < 1e-3  # all 64 rows: attention runs across the batch
+    res = eng.decode(max_steps=128, stop="batch")
+    assert res.n_steps == g["ids"].shape[1] - 1
+    n_full = check_ids(res.ids, g["ids"], g["margins"], tie=2e-4)
+    assert n_full >= 56, n_full
+    check_teacher_forced(eng, g["ids"], g["margins"], 2e-4, g["logits"])
+    eng.close()
+
+
+def test_config4_beam4_b32_256(pkg, golden):
+    g = golden("b384_k4_bench")
+    m = g["meta"]
+    K, S, P = m["K"], m["steps"], m["max_pos"]
+    assert (K, S) == (4, 256)
+    w = pkg.synth.make_weights(1234, "init", max_pos=P)
+    eng = pkg.Engine(img_hw=(384, 384), max_batch=32, precision="bf16x3", max_beam=K, max_pos=P)
+    eng.load_weights(w)
+    eng.encode(pkg.synth.make_images(32, 384, 384, seed0=1000))
+    res = eng.beam_search(beam=K, max_steps=S, stop="none")
+    assert res.n_steps == S
+    np.testing.assert_array_equal(res.beams[:2], g["seqs"])
+    np.testing.assert_allclose(res.scores[:2], g["scores"], rtol=1e-5, atol=1e-3)
+    assert (np.diff(res.scores, axis=1) <= 0).all()
+    # beam = 1 is greedy decoding, over all 32 rows and 256 steps
+    b1 = eng.beam_search(beam=1, max_steps=S, stop="none")
+    gr = eng.decode(max_steps=S, stop="none")
+    eos = pkg.synth.EOS_ID
+    for r in range(32):
+        row = gr.ids[r]
+        hit = np.flatnonzero(row[1:] == eos)
+        end = S + 1 if hit.size == 0 else int(hit[0]) + 2
+        np.testing.assert_array_equal(b1.ids[r, :end], row[:end])
+    again = eng.beam_search(beam=K, max_steps=S, stop="none")
+    np.testing.assert_array_equal(again.beams, res.beams)
+    eng.close()

@@ -21,8 +21,9 @@ def rel_err(a, b):
     return float(np.abs(a - b).max() / max(1.0, np.abs(b).max()))
 
 
-def make_engine(pkg, meta, max_batch=None, precision="fp32"):
-    eng = pkg.Engine(img_hw=(meta["H"], meta["W"]), max_batch=max_batch or meta.get("B", 1), precision=precision)
+def make_engine(pkg, meta, max_batch=None, precision="fp32", variant=()):
+    eng = pkg.Engine(img_hw=(meta["H"], meta["W"]), max_batch=max_batch or meta.get("B", 1), precision=precision,
+                     variant=variant)
     w = apply_eos_boost(pkg.synth.make_weights(meta["seed"], meta["variant"]), meta["eos_boost"])
     eng.load_weights(w)
     return eng, w
@@ -49,17 +50,15 @@ def test_encoder_stages_match_oracle(pkg, g384):
         assert e < 1e-4, f"features[{k}] rel err {e}"
 
 
-@pytest.mark.parametrize("env", [{}, {"MOCR_ATTN_FUSED": "0"}, {"MOCR_MLP_FUSED": "0", "MOCR_ATTN_FUSED": "0"}])
-def test_bf16x3_encoder_stages_match_oracle(pkg, golden, env, monkeypatch):
+@pytest.mark.parametrize("variant", [(), ("unfused_attn",), ("unfused_attn", "unfused_mlp")])
+def test_bf16x3_encoder_stages_match_oracle(pkg, golden, variant):
     """bf16x3 encoder stage by stage: the fused stage-1/2 attention half (wattn.hip) and
-    MLP half (mlp.hip), and the unfused kernels they replace (env A/B switches, read at
-    engine creation), all within 1e-4 of the fp32 oracle.  384x384: the stage-1 map is
-    96x96, padded to 98 (zero tokens) and rolled by 3 on odd blocks."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+    MLP half (mlp.hip), and the unfused kernels they replace (MOCR_VARIANT_* flags), all
+    within 1e-4 of the fp32 oracle.  384x384: the stage-1 map is 96x96, padded to 98
+    (zero tokens) and rolled by 3 on odd blocks."""
     g = golden("g384_b2_pert")
     m = g["meta"]
-    eng, w = make_engine(pkg, m, precision="bf16x3")
+    eng, w = make_engine(pkg, m, precision="bf16x3", variant=variant)
     imgs = pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m["img_kind"])
     _, stages = model_ref.encode(model_ref.build_model(w), torch.from_numpy(imgs), stages=True)
     eng.set_images(imgs)
@@ -95,6 +94,22 @@ def test_teacher_forced_logits_384(pkg, g384):
     assert err < LOGIT_TOL, err
     # argmax under teacher forcing reproduces the greedy ids
     np.testing.assert_array_equal(res.ids[:, 1:], g["ids"][:, 1:])
+
+
+def test_unfolded_decode_variant_matches_golden(pkg, golden):
+    """MOCR_VARIANT_DEC_UNFOLDED: the 8-kernel greedy step (LayerNorms applied by their
+    consumers) gives the fixture's ids and teacher-forced logits, as the folded step does."""
+    g = golden("g96x320_b4_eos")
+    m = g["meta"]
+    eng, _ = make_engine(pkg, m, variant=("dec_unfolded",))
+    eng.encode(pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m["img_kind"]))
+    res = eng.decode(max_steps=m["steps"], stop="batch")
+    np.testing.assert_array_equal(res.ids, g["ids"])
+    S = g["ids"].shape[1] - 1
+    tf = eng.decode(max_steps=S, stop="none", forced=g["ids"], want_logits=True)
+    n = g["logits"].shape[1]
+    assert float(np.abs(tf.logits[:, :n] - g["logits"]).max()) < LOGIT_TOL
+    eng.close()
 
 
 def test_decode_is_deterministic(pkg, g384):
@@ -223,4 +238,20 @@ def test_inference_predict_strings(pkg, golden):
     eng, _ = make_engine(pkg, dict(m, B=3))  # max_batch 3 < 4 images: chunked decode
     imgs = pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m["img_kind"])
     assert pkg.inference.predict(imgs, eng, vocab, idx2char, "cuda") == m["strings"]
+    eng.close()
+
+
+def test_predict_script_batch1(pkg, golden):
+    """src/predict.py predict(): one image at a time, stop at its own EOS, tokens
+    output_seq[1:-1] (sos and EOS dropped) -- each row of the 96x320 fixture."""
+    g = golden("g96x320_b4_eos")
+    m = g["meta"]
+    vocab, idx2char = pkg.synth.synthetic_vocab()
+    eng, _ = make_engine(pkg, dict(m, B=1))
+    imgs = pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m["img_kind"])
+    for r in range(m["B"]):
+        row = g["ids"][r]
+        e = int(np.flatnonzero(row[1:] == pkg.synth.EOS_ID)[0]) + 1  # column of the first EOS
+        expected = [idx2char[int(i)] for i in row[1:e]]
+        assert pkg.predict.predict(imgs[r:r + 1], eng, vocab, idx2char) == expected
     eng.close()

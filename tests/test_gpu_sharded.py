@@ -1,0 +1,106 @@
+"""GPU: the image-parallel path (BASELINE config 3) with the real engine.
+
+* two fresh processes share cuda:0 (this pool's boxes have one GPU), each encodes and
+  decodes its own shard of a fixture batch, and the token streams gathered over a host
+  process group (gloo) equal the fixture's ids -- the shard/gather logic of bench.py's
+  N>1 path with the engine in it;
+* the RCCL gather inside libmathocr.so (mocr_group_*) on a one-rank group: RCCL refuses
+  two ranks on one device, so its N>1 run is the driver's multi-GPU bench.
+"""
+import importlib
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q):
+    try:
+        sys.path.insert(0, REPO)
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        pkg = importlib.import_module("handwritten-math-ocr-api_amd")
+        from tests.conftest import load_golden
+        from oracle.gen_golden import apply_eos_boost
+        g = load_golden("g96x320_b4_eos")
+        m = g["meta"]
+        a, b = pkg.parallel.shard_bounds(m["B"], world, rank)
+        imgs = pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m["img_kind"])[a:b]
+        eng = pkg.Engine(img_hw=(m["H"], m["W"]), max_batch=b - a, precision="bf16x3", device=0)
+        eng.load_weights(apply_eos_boost(pkg.synth.make_weights(m["seed"], m["variant"]), m["eos_boost"]))
+        eng.encode(imgs)
+        steps = g["ids"].shape[1] - 1
+        res = eng.decode(max_steps=steps, stop="none")
+        eng.close()
+        gathered = pkg.parallel.gather_ids_host(torch.from_numpy(res.ids), world)
+        if rank == 0:
+            q.put(("ok", gathered.numpy()))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as ex:  # report instead of hanging the parent on the queue
+        q.put(("error", f"rank {rank}: {ex!r}"))
+        raise
+
+
+def test_two_shards_on_one_gpu_match_fixture(golden):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    status, out = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+    assert status == "ok", out
+    assert all(p.exitcode == 0 for p in procs)
+    # rows are independent: the fixed-length decode of each shard equals the fixture's rows
+    # (the fixture's batch-global stop only decides how many columns exist)
+    np.testing.assert_array_equal(out, golden("g96x320_b4_eos")["ids"])
+
+
+def test_rccl_group_gather_one_rank(pkg):
+    grp = pkg.parallel.RcclGroup(world=1, rank=0, device=0)
+    ids = torch.arange(64 * 129, dtype=torch.int32, device="cuda:0").reshape(64, 129)
+    out = grp.gather_ids(ids)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ids)
+    with pytest.raises(ValueError):
+        grp.gather_ids(ids.float())
+    grp.close()
+
+
+def test_rccl_gather_of_engine_ids(pkg, golden):
+    """decode_into writes the shard's ids to device memory; the group gathers them."""
+    from oracle.gen_golden import apply_eos_boost
+    g = golden("g96x320_b4_eos")
+    m = g["meta"]
+    eng = pkg.Engine(img_hw=(m["H"], m["W"]), max_batch=m["B"], precision="bf16x3", device=0)
+    eng.load_weights(apply_eos_boost(pkg.synth.make_weights(m["seed"], m["variant"]), m["eos_boost"]))
+    eng.encode(pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m["img_kind"]))
+    steps = g["ids"].shape[1] - 1
+    ids = torch.empty((m["B"], steps + 1), dtype=torch.int32, device="cuda:0")
+    eng.decode_into(ids, max_steps=steps, stop="none")
+    grp = pkg.parallel.RcclGroup(world=1, rank=0, device=0)
+    out = grp.gather_ids(ids)
+    np.testing.assert_array_equal(out.cpu().numpy(), g["ids"])
+    grp.close()
+    eng.close()

@@ -29,7 +29,7 @@ def _worker(rank, world, port, n_total, steps, q):
     a, b = pkg.parallel.shard_bounds(n_total, world, rank)
     # stand-in for this rank's decoded ids: row i of the global batch is filled with i
     local = torch.arange(a, b, dtype=torch.int32)[:, None].repeat(1, steps + 1)
-    gathered = pkg.parallel.gather_ids(local, world)
+    gathered = pkg.parallel.gather_ids_host(local, world)
     if rank == 0:
         q.put(gathered.numpy().tolist())
     dist.barrier()

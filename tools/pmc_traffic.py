@@ -7,8 +7,10 @@
 Corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts 64 B per 128-B request for
 wide (16 B/lane) streaming reads on gfx950, so it is doubled; WRITE_SIZE is taken as is
 (exact for 16 B/lane stores, uncalibrated for the 2-4 B/lane epilogue stores here).
-Both counters are in KiB.  Dispatches are mapped to the engine's kernel classes
-(engine.hip encode()) by their order in one encode.
+Both counters are in KiB.  Encoder dispatches are mapped to the engine's kernel classes
+(engine.hip encode()) by their order in one encode; every dispatch after the encoder
+(``profile_encoder.py --decode-steps N``: the embedding kernel, then N graph-captured
+greedy steps) is summed into ``decode.step`` (bytes per step) and listed per kernel.
 """
 import csv
 import os
@@ -16,14 +18,18 @@ import json
 import sys
 
 
-def classes_in_order(mlp_fused=()):
+def classes_in_order(mlp_fused=(), attn_fused=()):
     """Encoder dispatch classes in launch order; stages in `mlp_fused` run norm2 + MLP as one
-    kernel (mlp.hip) instead of layernorm, fc1, fc2."""
+    kernel (mlp.hip) instead of layernorm, fc1, fc2, and stages in `attn_fused` run norm1 +
+    qkv + W-MSA + proj as one kernel (wattn.hip)."""
     names = ["split(weights)", "split(kv-weights)", "stem"]
     depth = (2, 2, 6, 2)
     for s in range(4):
         for _ in range(depth[s]):
-            names += [f"s{s+1}.ln_partition", f"s{s+1}.qkv", f"s{s+1}.wattn", f"s{s+1}.proj"]
+            if s + 1 in attn_fused:
+                names += [f"s{s+1}.attn"]
+            else:
+                names += [f"s{s+1}.ln_partition", f"s{s+1}.qkv", f"s{s+1}.wattn", f"s{s+1}.proj"]
             names += [f"s{s+1}.mlp"] if s + 1 in mlp_fused else [f"s{s+1}.layernorm", f"s{s+1}.fc1", f"s{s+1}.fc2"]
         if s < 3:
             names += [f"merge{s+1}.ln", f"merge{s+1}"]
@@ -31,28 +37,56 @@ def classes_in_order(mlp_fused=()):
     return names
 
 
-def main(fetch_csv, write_csv, out):
-    # encoder dispatches only (the load-time decoder weight folding is not an encoder kernel)
+def main(fetch_csv, write_csv, out, decode_steps=0):
+    decode_steps = int(decode_steps)
+    # engine dispatches only (the load-time decoder weight folding is not an encoder kernel)
     keep = lambda r: "mocr" in r["Kernel_Name"] and "fold_mm" not in r["Kernel_Name"]
     f = [r for r in csv.DictReader(open(fetch_csv)) if keep(r)]
     w = [r for r in csv.DictReader(open(write_csv)) if keep(r)]
-    fused = sorted({1 if "mlp_fused_kernel<96" in r["Kernel_Name"] else 2 for r in f if "mlp_fused" in r["Kernel_Name"]})
-    names = classes_in_order(fused)
-    fp32 = len(f) == len(names) - 3  # fp32 mode has no bf16 split kernels
-    if fp32:
+    assert len(f) == len(w)
+    kn = [r["Kernel_Name"] for r in f]
+    fused = sorted({1 if "mlp_fused_kernel<96" in k else 2 for k in kn if "mlp_fused" in k})
+    afused = sorted({1 if "swin_attn_kernel<96" in k else 2 for k in kn if "swin_attn_kernel" in k})
+    names = classes_in_order(fused, afused)
+    if not any("split_bf16" in k for k in kn[:3]):  # fp32 mode has no bf16 split kernels
         names = [n for n in names if not n.startswith("split")]
-    assert len(f) == len(w) == len(names), (len(f), len(w), len(names))
+    n_enc = len(names)
+    assert len(f) >= n_enc, (len(f), n_enc)
+    if not decode_steps:
+        assert len(f) == n_enc, (len(f), n_enc)
     agg = {}
-    for name, a, b in zip(names, f, w):
+    dec_kernels = {}
+    for i, (a, b) in enumerate(zip(f, w)):
         assert a["Kernel_Name"] == b["Kernel_Name"]
+        fb = 2 * float(a["Counter_Value"]) * 1024
+        wb = float(b["Counter_Value"]) * 1024
+        if i < n_enc:
+            name = names[i]
+        else:
+            name = "decode.step"
+            k = a["Kernel_Name"].split("(")[0].replace("void ", "").replace("mocr::(anonymous namespace)::", "")
+            dk = dec_kernels.setdefault(k, {"launches": 0, "fetch_bytes": 0.0, "write_bytes": 0.0})
+            dk["launches"] += 1
+            dk["fetch_bytes"] += fb
+            dk["write_bytes"] += wb
         d = agg.setdefault(name, {"launches": 0, "fetch_bytes": 0.0, "write_bytes": 0.0, "kernel": a["Kernel_Name"]})
         d["launches"] += 1
-        d["fetch_bytes"] += 2 * float(a["Counter_Value"]) * 1024
-        d["write_bytes"] += float(b["Counter_Value"]) * 1024
+        d["fetch_bytes"] += fb
+        d["write_bytes"] += wb
     for d in agg.values():
         d["hbm_bytes_per_launch"] = (d["fetch_bytes"] + d["write_bytes"]) / d["launches"]
-    json.dump({"source": [os.path.relpath(p, os.path.dirname(os.path.abspath(out))) for p in (fetch_csv, write_csv)], "fetch_correction": 2.0, "classes": agg}, open(out, "w"), indent=1)
+    if decode_steps and "decode.step" in agg:
+        d = agg["decode.step"]
+        d["kernel"] = "greedy decode step (all dispatches after the encoder / steps)"
+        d["dispatches"] = d["launches"]
+        d["launches"] = decode_steps
+        d["hbm_bytes_per_launch"] = (d["fetch_bytes"] + d["write_bytes"]) / decode_steps
+        for dk in dec_kernels.values():
+            dk["hbm_bytes_per_launch"] = (dk["fetch_bytes"] + dk["write_bytes"]) / dk["launches"]
+    json.dump({"source": [os.path.relpath(p, os.path.dirname(os.path.abspath(out))) for p in (fetch_csv, write_csv)],
+               "fetch_correction": 2.0, "decode_steps": decode_steps, "classes": agg, "decode_kernels": dec_kernels},
+              open(out, "w"), indent=1)
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])
