@@ -64,7 +64,7 @@ def main(fetch_csv, write_csv, out, decode_steps=0):
             name = names[i]
         else:
             name = "decode.step"
-            k = a["Kernel_Name"].split("(")[0].replace("void ", "").replace("mocr::(anonymous namespace)::", "")
+            k = a["Kernel_Name"].replace("void ", "").replace("mocr::(anonymous namespace)::", "").split("(")[0]
             dk = dec_kernels.setdefault(k, {"launches": 0, "fetch_bytes": 0.0, "write_bytes": 0.0})
             dk["launches"] += 1
             dk["fetch_bytes"] += fb
