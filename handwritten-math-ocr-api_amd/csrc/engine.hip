@@ -1,5 +1,6 @@
 // libmathocr.so: engine state, weight layout, encoder schedule, hipGraph-captured
 // decode loop, and the C-ABI of include/mathocr.h.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1686,6 +1687,21 @@ int mocr_debug_encode_until(mocr_engine* eng, int batch, int k, float* host_out,
     eng->encode(batch, k);
     if (n != eng->stage_elems(k)) throw std::runtime_error("wrong output size for stage " + std::to_string(k));
     MOCR_HIP_CHECK(hipMemcpy(host_out, eng->X, n * sizeof(float), hipMemcpyDeviceToHost));
+  })
+}
+
+int mocr_set_cu_mask(mocr_engine* eng, const uint32_t* mask, int n_words) {
+  MOCR_API_BODY(eng, {
+    if (n_words < 0 || (n_words > 0 && !mask)) throw std::runtime_error("bad CU mask");
+    MOCR_HIP_CHECK(hipSetDevice(eng->device));
+    MOCR_HIP_CHECK(hipStreamSynchronize(eng->stream));
+    hipStream_t s = nullptr;
+    if (n_words)
+      MOCR_HIP_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)n_words, mask));
+    else
+      MOCR_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    MOCR_HIP_CHECK(hipStreamDestroy(eng->stream));
+    eng->stream = s;
   })
 }
 

@@ -73,6 +73,7 @@ def load_library(path: str = LIB_PATH):
         "mocr_debug_encode_until": (I, [P, I, I, f32p, SZ]),
         "mocr_set_timing": (I, [P, I]),
         "mocr_get_timing": (I, [P, ctypes.POINTER(KernelStat), I]),
+        "mocr_set_cu_mask": (I, [P, ctypes.POINTER(ctypes.c_uint32), I]),
         "mocr_group_unique_id": (I, [ctypes.c_char_p]),
         "mocr_group_create": (I, [ctypes.c_char_p, I, I, I, ctypes.POINTER(P)]),
         "mocr_group_destroy": (I, [P]),
@@ -93,7 +94,7 @@ def exported_symbols():
     return ["mocr_abi_version", "mocr_weight_count", "mocr_memory_tokens", "mocr_create", "mocr_destroy",
             "mocr_last_error", "mocr_load_weights", "mocr_set_images", "mocr_set_images_device", "mocr_encode",
             "mocr_get_memory", "mocr_decode", "mocr_decode_device", "mocr_decode_beam", "mocr_debug_encode_until",
-            "mocr_set_timing", "mocr_get_timing", "mocr_set_encoder_pos", "mocr_group_unique_id", "mocr_group_create",
+            "mocr_set_timing", "mocr_get_timing", "mocr_set_encoder_pos", "mocr_set_cu_mask", "mocr_group_unique_id", "mocr_group_create",
             "mocr_group_destroy", "mocr_group_last_error", "mocr_group_gather_ids"]
 
 
@@ -291,6 +292,19 @@ class Engine:
     def greedy(self, images, max_steps=150, stop="batch") -> DecodeResult:
         self.encode(images)
         return self.decode(max_steps, stop)
+
+    def set_cu_mask(self, cus=None):
+        """Run this engine's stream on the CUs in ``cus`` (iterable of CU indices; None:
+        all CUs)."""
+        if cus is None:
+            self._check(self.lib.mocr_set_cu_mask(self._h, None, 0), "mocr_set_cu_mask")
+            return
+        cus = list(cus)
+        words = (max(cus) // 32 + 1) if cus else 1
+        arr = (ctypes.c_uint32 * words)()
+        for c in cus:
+            arr[c // 32] |= 1 << (c % 32)
+        self._check(self.lib.mocr_set_cu_mask(self._h, arr, words), "mocr_set_cu_mask")
 
     # ------------------------------------------------------------------ timing
     def set_timing(self, enabled: bool):

@@ -179,6 +179,10 @@ typedef struct mocr_kernel_stat {
 } mocr_kernel_stat;
 
 int mocr_set_timing(mocr_engine* eng, int enabled); /* also resets the counters */
+
+/* Restrict the engine's HIP stream to a set of CUs (hipExtStreamCreateWithCUMask: bit i
+ * of mask[i / 32] enables CU i); n_words = 0 restores an unmasked stream. */
+int mocr_set_cu_mask(mocr_engine* eng, const uint32_t* mask, int n_words);
 int mocr_get_timing(mocr_engine* eng, mocr_kernel_stat* out, int max_records);
 
 /* ---- Image-parallel group (BASELINE config 3) ----------------
