@@ -293,7 +293,7 @@ def main():
         if rd:
             out["roofline_decode"] = rd
         out["encoder_ms_per_batch_events"] = sum(v["total_ms"] for k, v in iso["stats"].items()
-                                                 if not k.startswith("decode")) / 3
+                                                 if not k.startswith(("decode", "host"))) / 3
         out["kernel_classes"] = {k: {"launches": v["launches"], "avg_ms": v["total_ms"] / v["launches"],
                                      "tflops": v["flops"] / v["total_ms"] * 1e-9 if v["total_ms"] else None}
                                  for k, v in sorted(iso["stats"].items())}

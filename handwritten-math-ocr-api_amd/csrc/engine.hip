@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -1072,6 +1073,26 @@ struct mocr_engine {
           ap.wg = wg;
           timed(attn_n[s], 8.0 * rows * C * C + 4.0 * rows * kWinTok * C, 8.0 * rows * C + (dwl ? 4.0 : 2.0) * 4.0 * C * C,
                 [&] { launch_swin_attn_fused(ap, stream); });
+        } else if (b16 && attn_fused() && swin_attn_noproj_supported(C)) {
+          // norm1 + qkv + W-MSA in one kernel writing the ATT planes (wattn.hip), then proj
+          SwinAttnParams ap{};
+          ap.X = X;
+          ap.ln_g = W(w.n1w);
+          ap.ln_b = W(w.n1b);
+          ap.wqkv = dwh + w.qkvw;
+          ap.wqkv_lo = dwl ? dwl + w.qkvw : nullptr;
+          ap.bqkv = W(w.qkvb);
+          ap.table = relmask[bi];
+          ap.att_hi = ATTh;
+          ap.att_lo = dwl ? ATTl : nullptr;
+          ap.B = B;
+          ap.C = C;
+          ap.heads = g.heads;
+          ap.wg = wg;
+          timed(attn_n[s], 6.0 * rows * C * C + 4.0 * rows * kWinTok * C, 4.0 * rows * C + (dwl ? 4.0 : 2.0) * 3.0 * C * C +
+                (dwl ? 4.0 : 2.0) * rows * C, [&] { launch_swin_attn_noproj(ap, stream); });
+          gemm(proj_n[s], opATT, wop(w.projw), W(w.projb), X, nullptr, nullptr, (int)wrows, C, C, EPI_WINRES, &wg,
+               rows);
         } else {
           timed(ln1_n[s], 0, 8.0 * wrows * C,
                 [&] { launch_ln_partition(X, W(w.n1w), W(w.n1b), xw32, XWh, XWl, B, C, wg, stream); });
@@ -1449,8 +1470,15 @@ struct mocr_engine {
       MOCR_HIP_CHECK(hipEventRecord(t0, stream));
     }
     for (int c = 0; c < chunks; ++c) {
-      MOCR_HIP_CHECK(hipGraphLaunch(graph_for(B, c, max_steps, want_logits, forced_host != nullptr, stop_batch),
-                                    stream));
+      hipGraphExec_t ge = graph_for(B, c, max_steps, want_logits, forced_host != nullptr, stop_batch);
+      const auto h0 = std::chrono::steady_clock::now();
+      MOCR_HIP_CHECK(hipGraphLaunch(ge, stream));
+      if (timing) {  // host time spent submitting the chunk's graph
+        mocr_kernel_stat& hs_ = stats["host.graph_launch"];
+        std::strncpy(hs_.name, "host.graph_launch", sizeof(hs_.name) - 1);
+        hs_.launches += 1;
+        hs_.total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
+      }
       if (stop_batch && c + 1 < chunks) {
         MOCR_HIP_CHECK(hipMemcpyAsync(&hs, st, sizeof(hs), hipMemcpyDeviceToHost, stream));
         MOCR_HIP_CHECK(hipStreamSynchronize(stream));

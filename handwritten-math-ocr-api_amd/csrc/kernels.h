@@ -120,11 +120,15 @@ struct SwinAttnParams {
   const void *wproj, *wproj_lo;  // [C, C]
   const float* bproj;         // [C]
   const float* table;         // [4 window types][heads][64 q][64 key] bias + mask (build_relmask)
+  uint16_t *att_hi, *att_lo;  // noproj: O planes [B * nWin * 49, C] (window-token rows)
   int B, C, heads;
   WinGeom wg;
 };
 bool swin_attn_fused_supported(int C);
 void launch_swin_attn_fused(const SwinAttnParams& p, hipStream_t s);
+// norm1 + qkv + W-MSA only (no proj), O written for the proj GEMM (EPI_WINRES)
+bool swin_attn_noproj_supported(int C);
+void launch_swin_attn_noproj(const SwinAttnParams& p, hipStream_t s);
 
 // x -> bf16 hi (and lo) planes.
 void launch_split_bf16(const float* x, uint16_t* hi, uint16_t* lo, size_t n, hipStream_t s);

@@ -21,6 +21,14 @@
 //     as the B fragments of proj's k-step h; wave w computes out^T rows 32w .. 32w+31
 //     (A = W_proj rows, the same permuted k order), adds bias + residual and scatters
 //     to the window-reversed, un-rolled pixel (EPI_WINRES's mapping).
+//
+// Stage 3 (C = 384, 12 heads: swin_attn_noproj_kernel) keeps A-C and drops D: the LN'd
+// window alone fills 96 KB of LDS, so there is no room for proj's operands beside it.
+// The waves loop over the heads, keep the LN rows in LDS for the whole kernel, and write
+// O as bf16 hi / lo planes in window-token order -- the A operand of the proj GEMM
+// (EPI_WINRES), exactly as window_attention_mfma_kernel writes it.  That removes the
+// LN-partition kernel, the fp32 QKV round trip and the attention kernel's re-read
+// (s3, PMC: 864 MB -> 195 MB of HBM traffic per block before proj).
 #include "kernels.h"
 
 namespace mocr {
@@ -52,16 +60,22 @@ template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
-// sum over aligned groups of L lanes (L = 8, 16): quad_perm xor 1, xor 2, then
+// sum over aligned groups of L lanes (L = 8, 16, 32): quad_perm xor 1, xor 2, then
 // row_half_mirror / row_mirror, which pair each lane with one of the other half's
-// lanes, all of which hold the same partial sum by then (== __shfl_xor by 4, 8)
+// lanes, all of which hold the same partial sum by then (== __shfl_xor by 4, 8), then
+// (L = 32) the other 16-lane row by v_permlane16_swap (as swap16 below)
 template <int L>
 __device__ __forceinline__ float row_sum(float s) {
-  static_assert(L == 8 || L == 16, "row_sum: 8 or 16 lanes");
+  static_assert(L == 8 || L == 16 || L == 32, "row_sum: 8, 16 or 32 lanes");
   s += dpp<0xB1>(s);
   s += dpp<0x4E>(s);
   s += dpp<0x141>(s);
-  if constexpr (L == 16) s += dpp<0x140>(s);
+  if constexpr (L >= 16) s += dpp<0x140>(s);
+  if constexpr (L == 32) {
+    float a = s, b = s;
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    s = a + b;
+  }
   return s;
 }
 // x[lane ^ 16] and x[lane ^ 32] via v_permlane{16,32}_swap (VALU, no LDS queue).  The
@@ -430,6 +444,284 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
   }
 }
 
+// Stage 3: norm1 + qkv + W-MSA without proj (see the header): WAVES waves loop over the
+// heads, O goes to the ATT planes.
+template <int C, int PASSES, int OCC, int WAVES, int KU>
+__global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(OCC)))
+swin_attn_noproj_kernel(SwinAttnParams p) {
+  constexpr bool X3 = PASSES == 3;
+  constexpr int PL = X3 ? 2 : 1;
+  constexpr int HEADS = C / 32;  // = k-steps of every GEMM here
+  constexpr int NT = 64 * WAVES;
+  constexpr int RC = C / 8;      // 16-B chunks per LN row
+  // chunk c of row r at c ^ s(r): conflict-free ds_read_b128 fragment reads (mlp.hip W1 image)
+  constexpr int SW = (RC % 16 == 0) ? 16 : ((RC % 8 == 0) ? 8 : 4);
+  constexpr int SH = SW == 16 ? 0 : 1;
+  constexpr int XB = 64 * C * 2;  // bytes per plane: the LN'd window, later proj's B fragments
+  constexpr int LPR = C / 12;     // lanes per row in the LayerNorm (12 floats each)
+  static_assert(RC % SW == 0 && 64 % LPR == 0, "layout");
+  __shared__ __attribute__((aligned(16))) char lds[PL * XB];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int j16 = lane & 15;
+  const int g = lane >> 4;
+  const WinGeom& wg = p.wg;
+  const int b = (int)(blockIdx.x / (unsigned)wg.nWin);
+  const int win = (int)(blockIdx.x - (unsigned)b * wg.nWin);
+  const int wy = win / wg.nWx;
+  const int wx = win - wy * wg.nWx;
+  // X row of window token tk, -1 for the padded tokens and slots 49..63
+  auto pixel = [&](int tk) -> long {
+    const int ty = tk / kWin;
+    int y = wy * kWin + ty + wg.sh;
+    int x = wx * kWin + (tk - ty * kWin) + wg.sw;
+    if (y >= wg.pH) y -= wg.pH;
+    if (x >= wg.pW) x -= wg.pW;
+    return (tk < kWinTok && y < wg.H && x < wg.W) ? (long)(b * wg.H + y) * wg.W + x : -1L;
+  };
+
+  // ---- A: norm1 into LDS (ln_group_kernel's lanes per row and summation order; the xor
+  // reductions as DPP moves, which add the same pairs; 1/C and rsqrt as multiplies)
+  {
+    constexpr int RPP = NT / LPR;              // rows per pass (24; 16 at C = 384)
+    constexpr int NP = (64 + RPP - 1) / RPP;   // passes (3; 4)
+    const int gi = lane % LPR;
+    const int c0 = gi * 12;
+    float v[NP][12];
+    long px[NP];
+#pragma unroll
+    for (int ps = 0; ps < NP; ++ps) {  // every load first
+      px[ps] = pixel(ps * RPP + tid / LPR);
+      const float* src = p.X + (size_t)(px[ps] < 0 ? 0 : px[ps]) * C + c0;  // clamped, masked below
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        const floatx4 t = *reinterpret_cast<const floatx4*>(src + 4 * e);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[ps][4 * e + k] = t[k];
+      }
+    }
+    floatx4 gg[3], bb[3];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      gg[e] = *reinterpret_cast<const floatx4*>(p.ln_g + c0 + 4 * e);
+      bb[e] = *reinterpret_cast<const floatx4*>(p.ln_b + c0 + 4 * e);
+    }
+#pragma unroll
+    for (int ps = 0; ps < NP; ++ps) {
+      const int r = ps * RPP + tid / LPR;
+      float s = 0.f;
+#pragma unroll
+      for (int e = 0; e < 12; ++e) s += v[ps][e];
+      s = row_sum<LPR>(s);
+      const float mean = s * (1.0f / C);
+      float q = 0.f;
+#pragma unroll
+      for (int e = 0; e < 12; ++e) {
+        const float d = v[ps][e] - mean;
+        q += d * d;
+      }
+      q = row_sum<LPR>(q);
+      const float rstd = rsqrtf(q * (1.0f / C) + 1e-5f);
+      const bool zero = px[ps] < 0;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        float y[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) y[k] = zero ? 0.f : (v[ps][4 * e + k] - mean) * rstd * gg[e][k] + bb[e][k];
+        uint32_t h0, l0, h1, l1;
+        split2_bf16(y[0], y[1], h0, l0);
+        split2_bf16(y[2], y[3], h1, l1);
+        const int c = c0 + 4 * e;
+        const int off = r * (2 * C) + (((c >> 3) ^ ((r >> SH) & (SW - 1))) << 4) + ((c >> 2) & 1) * 8;
+        if (ps * RPP + RPP <= 64 || r < 64) {
+          *reinterpret_cast<uint2*>(lds + off) = make_uint2(h0, h1);
+          if constexpr (X3) *reinterpret_cast<uint2*>(lds + XB + off) = make_uint2(l0, l1);
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- B-C per head: k^T, v, q^T of head h, one 8-tile GEMM at a time (each converted
+  // to its attention fragments at once, so only one set of accumulators is live), then
+  // attention per 16-query tile
+  const uint16_t* wqh = static_cast<const uint16_t*>(p.wqkv);
+  const uint16_t* wql = static_cast<const uint16_t*>(p.wqkv_lo);
+  const float* bq = p.bqkv;
+  // LN fragment (tokens 16t + j16, channels 32ks + 8g ..): B of the k^T / q^T GEMMs, A of v's
+  auto xfrag = [&](int ks, int t, bf16x8(&f)[2]) {
+    const int r = 16 * t + j16;
+    const int off = r * (2 * C) + (((4 * ks + g) ^ ((r >> SH) & (SW - 1))) << 4);
+    f[0] = *reinterpret_cast<const bf16x8*>(lds + off);
+    if constexpr (X3) f[1] = *reinterpret_cast<const bf16x8*>(lds + XB + off);
+  };
+  // acc[f][t] = W[row0 + 16f + j16, :] . LN^T (features x tokens)
+  auto gemm_t = [&](int row0, floatx4(&acc)[2][4]) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[f][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll KU
+    for (int ks = 0; ks < HEADS; ++ks) {
+      bf16x8 w[2][2];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) wfrag<X3>(wqh, wql, C, row0 + 16 * f + j16, 32 * ks + 8 * g, w[f]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        bf16x8 xf[2];
+        xfrag(ks, t, xf);
+#pragma unroll
+        for (int f = 0; f < 2; ++f) acc[f][t] = mma<X3>(w[f], xf, acc[f][t]);
+      }
+    }
+  };
+
+#pragma unroll 1
+  for (int h = wave; h < HEADS; h += WAVES) {
+    bf16x8 kf[4][2], vf[2][2][2], qf4[4][2];
+    __builtin_amdgcn_s_setprio(1);
+    {
+      floatx4 acc[2][4];
+      gemm_t(C + 32 * h, acc);
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        float x[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          x[r] = acc[0][kt][r] + bq[C + 32 * h + 4 * g + r];
+          x[4 + r] = acc[1][kt][r] + bq[C + 32 * h + 16 + 4 * g + r];
+        }
+        pack8(x, kf[kt][0], kf[kt][1]);
+      }
+    }
+    {
+      // v [tokens x dims]: A = LN rows, B = W_v rows
+      floatx4 acc[4][2];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t][0] = acc[t][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll KU
+      for (int ks = 0; ks < HEADS; ++ks) {
+        bf16x8 w[2][2];
+#pragma unroll
+        for (int f = 0; f < 2; ++f) wfrag<X3>(wqh, wql, C, 2 * C + 32 * h + 16 * f + j16, 32 * ks + 8 * g, w[f]);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          bf16x8 xf[2];
+          xfrag(ks, t, xf);
+#pragma unroll
+          for (int f = 0; f < 2; ++f) acc[t][f] = mma<X3>(xf, w[f], acc[t][f]);
+        }
+      }
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const float bv = bq[2 * C + 32 * h + 16 * dt + j16];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          float x[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            x[r] = acc[2 * s][dt][r] + bv;
+            x[4 + r] = acc[2 * s + 1][dt][r] + bv;
+          }
+          pack8(x, vf[dt][s][0], vf[dt][s][1]);
+        }
+      }
+    }
+    {
+      floatx4 acc[2][4];
+      gemm_t(32 * h, acc);
+      const float scale = 0.17677669529663687f;  // 32 ** -0.5
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt) {
+        float x[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          x[r] = (acc[0][qt][r] + bq[32 * h + 4 * g + r]) * scale;
+          x[4 + r] = (acc[1][qt][r] + bq[32 * h + 16 + 4 * g + r]) * scale;
+        }
+        pack8(x, qf4[qt][0], qf4[qt][1]);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+
+    // ---- C: attention per 16-query tile
+    int type = 0;
+    if (wg.sh + wg.sw > 0) type = 2 * (wy == wg.nWin / wg.nWx - 1) + (wx == wg.nWx - 1);
+    const float* tb = p.table + ((size_t)type * HEADS + h) * 64 * 64;
+    floatx4 bm[4];  // bias + mask of the current query tile
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) bm[kt] = *reinterpret_cast<const floatx4*>(tb + j16 * 64 + 16 * kt + 4 * g);
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      if (qt > 0) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+          bm[kt] = *reinterpret_cast<const floatx4*>(tb + (16 * qt + j16) * 64 + 16 * kt + 4 * g);
+      }
+      floatx4 st[4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) st[kt] = mma<X3>(kf[kt], qf4[qt], floatx4{0.f, 0.f, 0.f, 0.f});
+      float m = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          st[kt][r] = st[kt][r] + bm[kt][r];
+          m = fmaxf(m, st[kt][r]);
+        }
+      }
+      m = xmax16_32(m);
+      float sum = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          st[kt][r] = __expf(st[kt][r] - m);
+          sum += st[kt][r];
+        }
+      sum = xsum16_32(sum);
+      bf16x8 pf[2][2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float x[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = st[2 * s + (j >> 2)][j & 3];
+        pack8(x, pf[s][0], pf[s][1]);
+      }
+      floatx4 o[2];
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        o[dt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) o[dt] = mma<X3>(vf[dt][s], pf[s], o[dt]);
+      }
+      // softmax normalisation after P.V (per query = per lane column)
+      const float inv = __builtin_amdgcn_rcpf(sum);
+      float x[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        x[r] = o[0][r] * inv;
+        x[4 + r] = o[1][r] * inv;
+      }
+      // ATT planes [window token row, C]: token 16qt + j16, channels 32h + {4g.., 16+4g..}
+      const int q = 16 * qt + j16;
+      if (q < kWinTok) {
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const size_t off = ((size_t)((long)b * wg.nWin + win) * kWinTok + q) * C + 32 * h + 16 * dt + 4 * g;
+          uint32_t h0, l0, h1, l1;
+          split2_bf16(x[4 * dt], x[4 * dt + 1], h0, l0);
+          split2_bf16(x[4 * dt + 2], x[4 * dt + 3], h1, l1);
+          *reinterpret_cast<uint2*>(p.att_hi + off) = make_uint2(h0, h1);
+          if constexpr (X3) *reinterpret_cast<uint2*>(p.att_lo + off) = make_uint2(l0, l1);
+        }
+      }
+    }
+  }
+}
+
 template <int C, int OCC>
 void launch_c(const SwinAttnParams& p, hipStream_t s) {
   const unsigned grid = (unsigned)((long)p.B * p.wg.nWin);
@@ -445,6 +737,7 @@ void launch_c(const SwinAttnParams& p, hipStream_t s) {
 }  // namespace
 
 bool swin_attn_fused_supported(int C) { return C == 96 || C == 192; }
+bool swin_attn_noproj_supported(int C) { return C == 384; }
 
 void launch_swin_attn_fused(const SwinAttnParams& p, hipStream_t s) {
   if (p.B <= 0) return;
@@ -456,6 +749,23 @@ void launch_swin_attn_fused(const SwinAttnParams& p, hipStream_t s) {
     case 192: launch_c<192, 2>(p, s); break;
     default: throw std::runtime_error("swin_attn: fused attention built for C = 96, 192");
   }
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_swin_attn_noproj(const SwinAttnParams& p, hipStream_t s) {
+  if (p.B <= 0) return;
+  if ((p.wqkv_lo == nullptr) != (p.att_lo == nullptr) || !p.att_hi)
+    throw std::runtime_error("swin_attn_noproj: ATT planes must match the weight planes");
+  if (p.heads * 32 != p.C) throw std::runtime_error("swin_attn: head dim must be 32");
+  if (p.C != 384) throw std::runtime_error("swin_attn_noproj: built for C = 384");
+  const unsigned grid = (unsigned)((long)p.B * p.wg.nWin);
+  // 12 waves (one head each, 3 per SIMD, 166 VGPRs) and k-steps unrolled by 2: 285 us per
+  // s3 block at B=64, 384² vs 313 (8 waves over the 12 heads, 2 per SIMD), 302 (8 waves,
+  // unroll 4), 318 (8 waves, no unroll)
+  if (p.wqkv_lo)
+    swin_attn_noproj_kernel<384, 3, 3, 12, 2><<<grid, 768, 0, s>>>(p);
+  else
+    swin_attn_noproj_kernel<384, 1, 3, 12, 2><<<grid, 768, 0, s>>>(p);
   MOCR_HIP_CHECK(hipGetLastError());
 }
 

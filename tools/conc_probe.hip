@@ -46,6 +46,19 @@ __global__ void __launch_bounds__(256) small_kernel(float* out, unsigned us) {
   if (threadIdx.x == 0) out[blockIdx.x] += lds[(blockIdx.x * 3) & 1023];
 }
 
+// memory streamers: each workgroup walks its slice of a large buffer `passes` times
+__global__ void __launch_bounds__(256) write_stream(float4* buf, size_t n, int passes) {
+  for (int p = 0; p < passes; ++p)
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+      buf[i] = make_float4((float)p, 0.f, 0.f, 0.f);
+}
+__global__ void __launch_bounds__(256) read_stream(const float4* buf, size_t n, int passes, float* out) {
+  float acc = 0.f;
+  for (int p = 0; p < passes; ++p)
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) acc += buf[i].x;
+  if (acc == 12345.f) out[0] = acc;
+}
+
 int main(int argc, char** argv) {
   const int tiles = 864;        // s3.fc1's 256x256 tiles
   const unsigned big_us = 80;   // per tile
@@ -100,6 +113,34 @@ int main(int argc, char** argv) {
     run(true, true, tiles);
     run(true, false, ncu);
     run(true, true, ncu);
+  }
+  // the small chain beside a memory streamer (writes dirty the L2s; reads do not)
+  {
+    const size_t n = (size_t)64 << 20;  // 1 GiB of float4
+    float4* buf;
+    CK(hipMalloc(&buf, n * sizeof(float4)));
+    CK(hipMemset(buf, 0, n * sizeof(float4)));
+    hipStream_t sm;
+    CK(hipStreamCreateWithFlags(&sm, hipStreamNonBlocking));
+    for (int mode = 0; mode < 3; ++mode) {
+      hipEvent_t s0, s1, m0, m1;
+      CK(hipEventCreate(&s0)); CK(hipEventCreate(&s1)); CK(hipEventCreate(&m0)); CK(hipEventCreate(&m1));
+      CK(hipDeviceSynchronize());
+      if (mode) {
+        CK(hipEventRecord(m0, sm));
+        if (mode == 1) write_stream<<<2048, 256, 0, sm>>>(buf, n, 3);
+        else read_stream<<<2048, 256, 0, sm>>>(buf, n, 3, ob);
+        CK(hipEventRecord(m1, sm));
+      }
+      CK(hipEventRecord(s0, ss));
+      CK(hipGraphLaunch(ge, ss));
+      CK(hipEventRecord(s1, ss));
+      CK(hipDeviceSynchronize());
+      float ts = 0, tm = 0;
+      CK(hipEventElapsedTime(&ts, s0, s1));
+      if (mode) CK(hipEventElapsedTime(&tm, m0, m1));
+      printf("small chain %s: %.3f ms (streamer %.3f ms)\n", mode == 0 ? "alone" : mode == 1 ? "|| write streamer" : "|| read streamer", ts, tm);
+    }
   }
   // N independent small chains on N streams: does the aggregate launch rate scale?
   for (int n = 1; n <= 8; n *= 2) {

@@ -50,6 +50,19 @@ def run(jobs):
 
 NE, ND = 30, 10
 res = {}
+# host time inside hipGraphLaunch per decode, alone and with 3 concurrent decoders
+for e in engs:
+    e.set_timing(True)
+run([(dec_loop, 4)])
+st = {k: v for k, v in engs[0].timing().items() if k.startswith("host") or k.startswith("decode")}
+print("alone", json.dumps(st), flush=True)
+for e in engs:
+    e.set_timing(True)
+run([(dec_loop, 4), (dec_loop, 4), (dec_loop, 4)])
+for e in engs:
+    st = {k: v for k, v in e.timing().items() if k.startswith("host") or k.startswith("decode")}
+    print("3 concurrent", json.dumps(st), flush=True)
+    e.set_timing(False)
 masks = {
     "hi32": (list(range(0, 224)), list(range(224, 256))),
     "stride8": ([i for i in range(256) if i % 8 != 7], [i for i in range(256) if i % 8 == 7]),

@@ -18,16 +18,19 @@ import json
 import sys
 
 
-def classes_in_order(mlp_fused=(), attn_fused=()):
+def classes_in_order(mlp_fused=(), attn_fused=(), attn_noproj=()):
     """Encoder dispatch classes in launch order; stages in `mlp_fused` run norm2 + MLP as one
-    kernel (mlp.hip) instead of layernorm, fc1, fc2, and stages in `attn_fused` run norm1 +
-    qkv + W-MSA + proj as one kernel (wattn.hip)."""
+    kernel (mlp.hip) instead of layernorm, fc1, fc2, stages in `attn_fused` run norm1 +
+    qkv + W-MSA + proj as one kernel (wattn.hip), stages in `attn_noproj` norm1 + qkv +
+    W-MSA as one kernel, then the proj GEMM."""
     names = ["split(weights)", "split(kv-weights)", "stem"]
     depth = (2, 2, 6, 2)
     for s in range(4):
         for _ in range(depth[s]):
             if s + 1 in attn_fused:
                 names += [f"s{s+1}.attn"]
+            elif s + 1 in attn_noproj:
+                names += [f"s{s+1}.attn", f"s{s+1}.proj"]
             else:
                 names += [f"s{s+1}.ln_partition", f"s{s+1}.qkv", f"s{s+1}.wattn", f"s{s+1}.proj"]
             names += [f"s{s+1}.mlp"] if s + 1 in mlp_fused else [f"s{s+1}.layernorm", f"s{s+1}.fc1", f"s{s+1}.fc2"]
@@ -47,7 +50,8 @@ def main(fetch_csv, write_csv, out, decode_steps=0):
     kn = [r["Kernel_Name"] for r in f]
     fused = sorted({1 if "mlp_fused_kernel<96" in k else 2 for k in kn if "mlp_fused" in k})
     afused = sorted({1 if "swin_attn_kernel<96" in k else 2 for k in kn if "swin_attn_kernel" in k})
-    names = classes_in_order(fused, afused)
+    anoproj = [3] if any("swin_attn_noproj_kernel" in k for k in kn) else []
+    names = classes_in_order(fused, afused, anoproj)
     if not any("split_bf16" in k for k in kn[:3]):  # fp32 mode has no bf16 split kernels
         names = [n for n in names if not n.startswith("split")]
     n_enc = len(names)
