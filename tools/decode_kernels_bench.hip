@@ -1,10 +1,12 @@
 // Per-kernel cost of each decode kernel of libmathocr.so, in a 200-long chain replayed
-// from a hipGraph (B = 64 rows, d = 256, max_pos = 150, M = 144, V = 5075, step t = 100).
+// from a hipGraph (B = 64 rows, d = 256, max_pos = 150, M = 144, V = 5075, step t = 100);
+// `decode_kernels_bench N` replays each chain on N streams at once (replica contention).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/decode_kernels_bench.hip
 //        -L handwritten-math-ocr-api_amd/lib -lmathocr -Wl,-rpath,$PWD/handwritten-math-ocr-api_amd/lib
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <functional>
 #include <string>
 #include <vector>
@@ -30,7 +32,8 @@ T* alloc(size_t n) {
   return (T*)p;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const int NS = argc > 1 ? atoi(argv[1]) : 1;  // concurrent streams replaying each chain
   const int B = 64, d = 256, P = 150, M = 144, V = 5075, Vp = 5088, t = 100, L = 8;
   float* x = alloc<float>(B * 512);
   float* y = alloc<float>(B * 512);
@@ -144,16 +147,28 @@ int main() {
     CK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
     CK(hipGraphLaunch(exec, s));
     CK(hipStreamSynchronize(s));
-    hipEvent_t e0, e1;
-    CK(hipEventCreate(&e0));
-    CK(hipEventCreate(&e1));
-    CK(hipEventRecord(e0, s));
-    for (int r = 0; r < 5; ++r) CK(hipGraphLaunch(exec, s));
-    CK(hipEventRecord(e1, s));
-    CK(hipEventSynchronize(e1));
-    float ms;
-    CK(hipEventElapsedTime(&ms, e0, e1));
-    printf("%-28s %.2f us per kernel\n", c.first.c_str(), ms * 1000.f / (5 * chain));
+    std::vector<hipStream_t> sts(NS);
+    std::vector<hipEvent_t> e0(NS), e1(NS);
+    for (int i = 0; i < NS; ++i) {
+      CK(hipStreamCreateWithFlags(&sts[i], hipStreamNonBlocking));
+      CK(hipEventCreate(&e0[i]));
+      CK(hipEventCreate(&e1[i]));
+    }
+    for (int i = 0; i < NS; ++i) {
+      CK(hipEventRecord(e0[i], sts[i]));
+      for (int r = 0; r < 5; ++r) CK(hipGraphLaunch(exec, sts[i]));
+      CK(hipEventRecord(e1[i], sts[i]));
+    }
+    float worst = 0.f;
+    for (int i = 0; i < NS; ++i) {
+      CK(hipEventSynchronize(e1[i]));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0[i], e1[i]));
+      worst = ms > worst ? ms : worst;
+    }
+    printf("%-34s %.2f us per kernel (%d concurrent stream%s)\n", c.first.c_str(), worst * 1000.f / (5 * chain), NS,
+           NS > 1 ? "s" : "");
+    for (int i = 0; i < NS; ++i) CK(hipStreamDestroy(sts[i]));
     CK(hipGraphExecDestroy(exec));
     CK(hipGraphDestroy(graph));
   }
