@@ -122,14 +122,18 @@ int main(int argc, char** argv) {
     CK(hipMemset(buf, 0, n * sizeof(float4)));
     hipStream_t sm;
     CK(hipStreamCreateWithFlags(&sm, hipStreamNonBlocking));
-    for (int mode = 0; mode < 3; ++mode) {
+    for (int mode = 0; mode < 5; ++mode) {
       hipEvent_t s0, s1, m0, m1;
       CK(hipEventCreate(&s0)); CK(hipEventCreate(&s1)); CK(hipEventCreate(&m0)); CK(hipEventCreate(&m1));
       CK(hipDeviceSynchronize());
       if (mode) {
         CK(hipEventRecord(m0, sm));
+        // modes 3 / 4: a 2 MiB buffer (L2-resident) written / read 3000 times: dirty L2 lines
+        // (or clean hits) without HBM bandwidth
         if (mode == 1) write_stream<<<2048, 256, 0, sm>>>(buf, n, 3);
-        else read_stream<<<2048, 256, 0, sm>>>(buf, n, 3, ob);
+        else if (mode == 2) read_stream<<<2048, 256, 0, sm>>>(buf, n, 3, ob);
+        else if (mode == 3) write_stream<<<2048, 256, 0, sm>>>(buf, (size_t)1 << 17, 3000);
+        else read_stream<<<2048, 256, 0, sm>>>(buf, (size_t)1 << 17, 3000, ob);
         CK(hipEventRecord(m1, sm));
       }
       CK(hipEventRecord(s0, ss));
@@ -139,7 +143,9 @@ int main(int argc, char** argv) {
       float ts = 0, tm = 0;
       CK(hipEventElapsedTime(&ts, s0, s1));
       if (mode) CK(hipEventElapsedTime(&tm, m0, m1));
-      printf("small chain %s: %.3f ms (streamer %.3f ms)\n", mode == 0 ? "alone" : mode == 1 ? "|| write streamer" : "|| read streamer", ts, tm);
+      const char* nm[] = {"alone", "|| HBM write streamer", "|| HBM read streamer", "|| L2-resident writer",
+                          "|| L2-resident reader"};
+      printf("small chain %s: %.3f ms (streamer %.3f ms)\n", nm[mode], ts, tm);
     }
   }
   // N independent small chains on N streams: does the aggregate launch rate scale?
