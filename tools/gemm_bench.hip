@@ -1,6 +1,5 @@
-// Standalone timing of libmathocr's bf16 / bf16x3 GEMM for one shape (HIP events), for
-// fast iteration and PMC runs on the encoder GEMM.  Variants come from the library's
-// environment switches (MOCR_GEMM_RING, MOCR_GEMM_BIG_MIN).
+// Standalone timing of libmathocr's bf16 / bf16x3 GEMM for one shape (HIP events) with an
+// output checksum, for fast iteration and PMC runs on the encoder GEMM shapes.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/gemm_bench.hip
 //        -L handwritten-math-ocr-api_amd/lib -lmathocr -Wl,-rpath,<repo>/handwritten-math-ocr-api_amd/lib
 // Run:   tools/gemm_bench M N K passes epi iters   (epi 0 store, 1 gelu, 2 resadd)
