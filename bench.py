@@ -163,13 +163,23 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = max(1, torch.cuda.device_count())  # counting devices does not initialise the GPU
+    shared = int(os.environ.get("LOCAL_WORLD_SIZE", "1")) > ndev  # ranks share a device (1-GPU test box)
+    local = local % ndev
     dev = f"cuda:{local}"
     pkg = importlib.import_module("handwritten-math-ocr-api_amd")
     grp = None
+    gather = "none"
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("gloo")  # host-side control only
-        grp = pkg.parallel.RcclGroup(world, rank, local)  # RCCL inside libmathocr.so
+        if shared:
+            # RCCL refuses two ranks on one device: the 33 KB token streams go over the host
+            # group instead (only on a box with fewer GPUs than ranks; tests/test_gpu_sharded.py)
+            gather = "gloo host (ranks share a device)"
+        else:
+            grp = pkg.parallel.RcclGroup(world, rank, local)  # RCCL inside libmathocr.so
+            gather = "rccl (mocr_group_gather_ids)"
     H, W = args.image
     B, S, R = args.batch, args.tokens, args.replicas
     dtype = DTYPE[args.precision]
@@ -205,6 +215,8 @@ def main():
         for ids, dt in pool.imap(step, range(n)):
             if grp:
                 grp.gather_ids(ids)  # RCCL all-gather of the token streams, in step order
+            elif world > 1:
+                pkg.parallel.gather_ids_host(ids.cpu(), world)
             lat.append(dt)
         return lat
 
@@ -281,7 +293,7 @@ def main():
                                f"{'beam' + str(args.beam) if args.beam else 'greedy'}@{S}, per GPU",
                    "global_batch": world * B,
                    "per_gpu_batch": B, "image": [H, W], "max_tokens": S, "vocab": pkg.synth.VOCAB,
-                   "decoder_layers": pkg.synth.N_LAYERS, "parallelism": f"image-parallel x{world}",
+                   "decoder_layers": pkg.synth.N_LAYERS, "parallelism": f"image-parallel x{world}", "gather": gather,
                    "replicas_per_gpu": R, "precision": args.precision},
         "p50_image_latency_ms": statistics.median(lat) * 1e3,
     }

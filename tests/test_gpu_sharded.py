@@ -104,3 +104,22 @@ def test_rccl_gather_of_engine_ids(pkg, golden):
     np.testing.assert_array_equal(out.cpu().numpy(), g["ids"])
     grp.close()
     eng.close()
+
+
+def test_bench_two_ranks_torchrun():
+    """bench.py's N > 1 path under torch.distributed.run (2 ranks; on a one-GPU box both
+    share cuda:0, so the token streams are gathered over the host group): one JSON line
+    from rank 0 with the whole-job throughput."""
+    import json
+    import subprocess
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--replicas", "1", "--no-isolated", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["value"] > 0 and out["config"]["global_batch"] == 128
+    assert out["config"]["gather"] in ("rccl (mocr_group_gather_ids)", "gloo host (ranks share a device)")
