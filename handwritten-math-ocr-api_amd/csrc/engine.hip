@@ -232,7 +232,8 @@ void check_config(const mocr_config& c) {
   req(c.precision == MOCR_PRECISION_FP32 || c.precision == MOCR_PRECISION_BF16 ||
           c.precision == MOCR_PRECISION_BF16X3,
       "precision");
-  req((c.variant & ~(MOCR_VARIANT_UNFUSED_ATTN | MOCR_VARIANT_UNFUSED_MLP | MOCR_VARIANT_DEC_UNFOLDED)) == 0,
+  req((c.variant & ~(MOCR_VARIANT_UNFUSED_ATTN | MOCR_VARIANT_UNFUSED_MLP | MOCR_VARIANT_DEC_UNFOLDED |
+                      MOCR_VARIANT_S4_FUSED_ATTN)) == 0,
       "variant: unknown MOCR_VARIANT_* flag");
   req(c.sos_id >= 0 && c.sos_id < c.vocab && c.eos_id >= 0 && c.eos_id < c.vocab, "special ids");
 }
@@ -966,6 +967,12 @@ struct mocr_engine {
   bool attn_fused() const { return !(cfg.variant & MOCR_VARIANT_UNFUSED_ATTN); }
   bool mlp_fused() const { return !(cfg.variant & MOCR_VARIANT_UNFUSED_MLP); }
   bool fold_greedy() const { return !(cfg.variant & MOCR_VARIANT_DEC_UNFOLDED); }
+  // stage 3 always (285 vs 301 us per block unfused at B=64, 384²); stage 4 only on request
+  // (258 vs 211 us: a window's 64 padded rows re-read all of W_qkv, 1.8 GB from L2 per block,
+  // and the padding costs 1.3x the GEMM's MFMA work)
+  bool noproj_fused(int C) const {
+    return attn_fused() && swin_attn_noproj_supported(C) && (C != 768 || (cfg.variant & MOCR_VARIANT_S4_FUSED_ATTN));
+  }
   int attn_passes() const {
     return cfg.precision == MOCR_PRECISION_FP32 ? 0 : (cfg.precision == MOCR_PRECISION_BF16X3 ? 3 : 1);
   }
@@ -1073,7 +1080,7 @@ struct mocr_engine {
           ap.wg = wg;
           timed(attn_n[s], 8.0 * rows * C * C + 4.0 * rows * kWinTok * C, 8.0 * rows * C + (dwl ? 4.0 : 2.0) * 4.0 * C * C,
                 [&] { launch_swin_attn_fused(ap, stream); });
-        } else if (b16 && attn_fused() && swin_attn_noproj_supported(C)) {
+        } else if (b16 && noproj_fused(C)) {
           // norm1 + qkv + W-MSA in one kernel writing the ATT planes (wattn.hip), then proj
           SwinAttnParams ap{};
           ap.X = X;

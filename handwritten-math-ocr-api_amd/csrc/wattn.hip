@@ -66,14 +66,19 @@ __device__ __forceinline__ float dpp(float v) {
 // (L = 32) the other 16-lane row by v_permlane16_swap (as swap16 below)
 template <int L>
 __device__ __forceinline__ float row_sum(float s) {
-  static_assert(L == 8 || L == 16 || L == 32, "row_sum: 8, 16 or 32 lanes");
+  static_assert(L == 8 || L == 16 || L == 32 || L == 64, "row_sum: 8, 16, 32 or 64 lanes");
   s += dpp<0xB1>(s);
   s += dpp<0x4E>(s);
   s += dpp<0x141>(s);
   if constexpr (L >= 16) s += dpp<0x140>(s);
-  if constexpr (L == 32) {
+  if constexpr (L >= 32) {
     float a = s, b = s;
     asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    s = a + b;
+  }
+  if constexpr (L == 64) {
+    float a = s, b = s;
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
     s = a + b;
   }
   return s;
@@ -446,6 +451,84 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
 
 // Stage 3: norm1 + qkv + W-MSA without proj (see the header): WAVES waves loop over the
 // heads, O goes to the ATT planes.
+// C of the no-proj kernels: attention of one head (K, V^T, Q^T fragments as B leaves
+// them) per 16-query tile; O goes to the ATT planes [window token row, C] at channels
+// ch0 + {4g.., 16+4g..} (tok0 = the window's first row)
+template <bool X3, int C>
+__device__ __forceinline__ void attend_to_planes(const bf16x8 (&kf)[4][2], const bf16x8 (&vf)[2][2][2],
+                                                 const bf16x8 (&qf4)[4][2], const float* tb, int j16, int g,
+                                                 size_t tok0, int ch0, uint16_t* att_hi, uint16_t* att_lo) {
+  floatx4 bm[4];  // bias + mask of the current query tile
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt) bm[kt] = *reinterpret_cast<const floatx4*>(tb + j16 * 64 + 16 * kt + 4 * g);
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {
+    if (qt > 0) {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+        bm[kt] = *reinterpret_cast<const floatx4*>(tb + (16 * qt + j16) * 64 + 16 * kt + 4 * g);
+    }
+    floatx4 st[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) st[kt] = mma<X3>(kf[kt], qf4[qt], floatx4{0.f, 0.f, 0.f, 0.f});
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        st[kt][r] = st[kt][r] + bm[kt][r];
+        m = fmaxf(m, st[kt][r]);
+      }
+    }
+    m = xmax16_32(m);
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        st[kt][r] = __expf(st[kt][r] - m);
+        sum += st[kt][r];
+      }
+    sum = xsum16_32(sum);
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = st[2 * s + (j >> 2)][j & 3];
+      pack8(x, pf[s][0], pf[s][1]);
+    }
+    floatx4 o[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      o[dt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) o[dt] = mma<X3>(vf[dt][s], pf[s], o[dt]);
+    }
+    // softmax normalisation after P.V (per query = per lane column)
+    const float inv = __builtin_amdgcn_rcpf(sum);
+    float x[8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      x[r] = o[0][r] * inv;
+      x[4 + r] = o[1][r] * inv;
+    }
+    // ATT planes [window token row, C]: token 16qt + j16, channels 32h + {4g.., 16+4g..}
+    const int q = 16 * qt + j16;
+    if (q < kWinTok) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const size_t off = (tok0 + q) * C + ch0 + 16 * dt + 4 * g;
+        uint32_t h0, l0, h1, l1;
+        split2_bf16(x[4 * dt], x[4 * dt + 1], h0, l0);
+        split2_bf16(x[4 * dt + 2], x[4 * dt + 3], h1, l1);
+        *reinterpret_cast<uint2*>(att_hi + off) = make_uint2(h0, h1);
+        if constexpr (X3) *reinterpret_cast<uint2*>(att_lo + off) = make_uint2(l0, l1);
+      }
+    }
+  }
+}
+
 template <int C, int PASSES, int OCC, int WAVES, int KU>
 __global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(OCC)))
 swin_attn_noproj_kernel(SwinAttnParams p) {
@@ -649,77 +732,216 @@ swin_attn_noproj_kernel(SwinAttnParams p) {
     // ---- C: attention per 16-query tile
     int type = 0;
     if (wg.sh + wg.sw > 0) type = 2 * (wy == wg.nWin / wg.nWx - 1) + (wx == wg.nWx - 1);
-    const float* tb = p.table + ((size_t)type * HEADS + h) * 64 * 64;
-    floatx4 bm[4];  // bias + mask of the current query tile
+    attend_to_planes<X3, C>(kf, vf, qf4, p.table + ((size_t)type * HEADS + h) * 64 * 64, j16, g,
+                            (size_t)((long)b * wg.nWin + win) * kWinTok, 32 * h, p.att_hi, p.att_lo);
+  }
+}
+
+// Stage 4 (C = 768, 24 heads): the LN'd window would take 192 KB of LDS, so the channels
+// go through LDS in two halves of 384.  Each workgroup owns HPG heads of one window (one
+// per wave) and keeps the head's k^T, v and q^T accumulators in registers across both
+// halves: A0 the row statistics over all 768 channels, then per half A (normalise the
+// half into LDS) and B (the half's 12 k-steps of the three GEMMs), then C as above.
+template <int C, int PASSES, int OCC, int HPG, int KU>
+__global__ void __launch_bounds__(64 * HPG) __attribute__((amdgpu_waves_per_eu(OCC)))
+swin_attn_noproj_ks_kernel(SwinAttnParams p) {
+  constexpr bool X3 = PASSES == 3;
+  constexpr int PL = X3 ? 2 : 1;
+  constexpr int HEADS = C / 32;
+  constexpr int NG = HEADS / HPG;  // workgroups per window
+  constexpr int NT = 64 * HPG;
+  constexpr int KC = 384;          // channels per LDS half
+  constexpr int NKC = C / KC;
+  constexpr int KS = KC / 32;      // k-steps per half
+  constexpr int RC = KC / 8;
+  constexpr int SW = (RC % 16 == 0) ? 16 : ((RC % 8 == 0) ? 8 : 4);
+  constexpr int SH = SW == 16 ? 0 : 1;
+  constexpr int XB = 64 * KC * 2;
+  constexpr int LPR = KC / 12;     // lanes per row of a half (12 floats each)
+  static_assert(HEADS % HPG == 0 && C % KC == 0 && RC % SW == 0 && 64 % LPR == 0 && C == 64 * 12, "layout");
+  __shared__ __attribute__((aligned(16))) char lds[PL * XB];
+  __shared__ float2 stats[64];  // (mean, rstd) per window row
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int j16 = lane & 15;
+  const int g = lane >> 4;
+  const WinGeom& wg = p.wg;
+  const unsigned wgi = blockIdx.x / (unsigned)NG;
+  const int hg = (int)(blockIdx.x - wgi * NG);
+  const int b = (int)(wgi / (unsigned)wg.nWin);
+  const int win = (int)(wgi - (unsigned)b * wg.nWin);
+  const int wy = win / wg.nWx;
+  const int wx = win - wy * wg.nWx;
+  auto pixel = [&](int tk) -> long {
+    const int ty = tk / kWin;
+    int y = wy * kWin + ty + wg.sh;
+    int x = wx * kWin + (tk - ty * kWin) + wg.sw;
+    if (y >= wg.pH) y -= wg.pH;
+    if (x >= wg.pW) x -= wg.pW;
+    return (tk < kWinTok && y < wg.H && x < wg.W) ? (long)(b * wg.H + y) * wg.W + x : -1L;
+  };
+
+  // ---- A0: mean and rstd of each row over the 768 channels (one wave per row, 12 each)
+#pragma unroll 1
+  for (int r = wave; r < 64; r += HPG) {
+    const long px = pixel(r);
+    const float* src = p.X + (size_t)(px < 0 ? 0 : px) * C + 12 * lane;
+    float v[12];
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt) bm[kt] = *reinterpret_cast<const floatx4*>(tb + j16 * 64 + 16 * kt + 4 * g);
+    for (int e = 0; e < 3; ++e) {
+      const floatx4 t = *reinterpret_cast<const floatx4*>(src + 4 * e);
 #pragma unroll
-    for (int qt = 0; qt < 4; ++qt) {
-      if (qt > 0) {
+      for (int k = 0; k < 4; ++k) v[4 * e + k] = t[k];
+    }
+    float s = 0.f;
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
-          bm[kt] = *reinterpret_cast<const floatx4*>(tb + (16 * qt + j16) * 64 + 16 * kt + 4 * g);
+    for (int e = 0; e < 12; ++e) s += v[e];
+    const float mean = row_sum<64>(s) * (1.0f / C);
+    float q = 0.f;
+#pragma unroll
+    for (int e = 0; e < 12; ++e) {
+      const float d = v[e] - mean;
+      q += d * d;
+    }
+    const float rstd = rsqrtf(row_sum<64>(q) * (1.0f / C) + 1e-5f);
+    if (lane == 0) stats[r] = make_float2(mean, rstd);
+  }
+
+  const int h = hg * HPG + wave;  // this wave's head
+  const uint16_t* wqh = static_cast<const uint16_t*>(p.wqkv);
+  const uint16_t* wql = static_cast<const uint16_t*>(p.wqkv_lo);
+  const float* bq = p.bqkv;
+  auto xfrag = [&](int ks, int t, bf16x8(&f)[2]) {
+    const int r = 16 * t + j16;
+    const int off = r * (2 * KC) + (((4 * ks + g) ^ ((r >> SH) & (SW - 1))) << 4);
+    f[0] = *reinterpret_cast<const bf16x8*>(lds + off);
+    if constexpr (X3) f[1] = *reinterpret_cast<const bf16x8*>(lds + XB + off);
+  };
+  // acc[f][t] += W[row0 + 16f + j16, k0 ..] . LN_half^T
+  auto gemm_t = [&](int row0, int k0, floatx4(&acc)[2][4]) {
+#pragma unroll KU
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 w[2][2];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) wfrag<X3>(wqh, wql, C, row0 + 16 * f + j16, k0 + 32 * ks + 8 * g, w[f]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        bf16x8 xf[2];
+        xfrag(ks, t, xf);
+#pragma unroll
+        for (int f = 0; f < 2; ++f) acc[f][t] = mma<X3>(w[f], xf, acc[f][t]);
       }
-      floatx4 st[4];
+    }
+  };
+  floatx4 ak[2][4], aq[2][4], av[4][2];
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) st[kt] = mma<X3>(kf[kt], qf4[qt], floatx4{0.f, 0.f, 0.f, 0.f});
-      float m = -INFINITY;
+  for (int f = 0; f < 2; ++f)
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
+    for (int t = 0; t < 4; ++t) ak[f][t] = aq[f][t] = av[t][f] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll 1
+  for (int kc = 0; kc < NKC; ++kc) {
+    __syncthreads();  // stats written (kc = 0) / the previous half's fragments read
+    // ---- A: channels [KC kc, KC kc + KC) of the LN'd rows into LDS
+    {
+      constexpr int RPP = NT / LPR;
+      constexpr int NP = (64 + RPP - 1) / RPP;
+      const int gi = lane % LPR;
+      const int c0 = gi * 12;
+      const int cg = kc * KC + c0;
+#pragma unroll 1
+      for (int ps = 0; ps < NP; ++ps) {
+        const int r = ps * RPP + tid / LPR;
+        if (ps * RPP + RPP <= 64 || r < 64) {
+          const long px = pixel(r);
+          const float* src = p.X + (size_t)(px < 0 ? 0 : px) * C + cg;
+          const float2 st = stats[r];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          st[kt][r] = st[kt][r] + bm[kt][r];
-          m = fmaxf(m, st[kt][r]);
-        }
-      }
-      m = xmax16_32(m);
-      float sum = 0.f;
+          for (int e = 0; e < 3; ++e) {
+            const floatx4 t = *reinterpret_cast<const floatx4*>(src + 4 * e);
+            const floatx4 gg = *reinterpret_cast<const floatx4*>(p.ln_g + cg + 4 * e);
+            const floatx4 bb = *reinterpret_cast<const floatx4*>(p.ln_b + cg + 4 * e);
+            float y[4];
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          st[kt][r] = __expf(st[kt][r] - m);
-          sum += st[kt][r];
-        }
-      sum = xsum16_32(sum);
-      bf16x8 pf[2][2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        float x[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) x[j] = st[2 * s + (j >> 2)][j & 3];
-        pack8(x, pf[s][0], pf[s][1]);
-      }
-      floatx4 o[2];
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        o[dt] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 2; ++s) o[dt] = mma<X3>(vf[dt][s], pf[s], o[dt]);
-      }
-      // softmax normalisation after P.V (per query = per lane column)
-      const float inv = __builtin_amdgcn_rcpf(sum);
-      float x[8];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        x[r] = o[0][r] * inv;
-        x[4 + r] = o[1][r] * inv;
-      }
-      // ATT planes [window token row, C]: token 16qt + j16, channels 32h + {4g.., 16+4g..}
-      const int q = 16 * qt + j16;
-      if (q < kWinTok) {
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          const size_t off = ((size_t)((long)b * wg.nWin + win) * kWinTok + q) * C + 32 * h + 16 * dt + 4 * g;
-          uint32_t h0, l0, h1, l1;
-          split2_bf16(x[4 * dt], x[4 * dt + 1], h0, l0);
-          split2_bf16(x[4 * dt + 2], x[4 * dt + 3], h1, l1);
-          *reinterpret_cast<uint2*>(p.att_hi + off) = make_uint2(h0, h1);
-          if constexpr (X3) *reinterpret_cast<uint2*>(p.att_lo + off) = make_uint2(l0, l1);
+            for (int k = 0; k < 4; ++k) y[k] = px < 0 ? 0.f : (t[k] - st.x) * st.y * gg[k] + bb[k];
+            uint32_t h0, l0, h1, l1;
+            split2_bf16(y[0], y[1], h0, l0);
+            split2_bf16(y[2], y[3], h1, l1);
+            const int c = c0 + 4 * e;
+            const int off = r * (2 * KC) + (((c >> 3) ^ ((r >> SH) & (SW - 1))) << 4) + ((c >> 2) & 1) * 8;
+            *reinterpret_cast<uint2*>(lds + off) = make_uint2(h0, h1);
+            if constexpr (X3) *reinterpret_cast<uint2*>(lds + XB + off) = make_uint2(l0, l1);
+          }
         }
       }
     }
+    __syncthreads();
+    // ---- B: this half's k-steps of k^T, v, q^T for head h
+    __builtin_amdgcn_s_setprio(1);
+    const int k0 = kc * KC;
+    gemm_t(C + 32 * h, k0, ak);
+#pragma unroll KU
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 w[2][2];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) wfrag<X3>(wqh, wql, C, 2 * C + 32 * h + 16 * f + j16, k0 + 32 * ks + 8 * g, w[f]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        bf16x8 xf[2];
+        xfrag(ks, t, xf);
+#pragma unroll
+        for (int f = 0; f < 2; ++f) av[t][f] = mma<X3>(xf, w[f], av[t][f]);
+      }
+    }
+    gemm_t(32 * h, k0, aq);
+    __builtin_amdgcn_s_setprio(0);
   }
+
+  // biases, scale, and the accumulators as attention operands (as swin_attn_noproj_kernel)
+  bf16x8 kf[4][2], vf[2][2][2], qf4[4][2];
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt) {
+    float x[8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      x[r] = ak[0][kt][r] + bq[C + 32 * h + 4 * g + r];
+      x[4 + r] = ak[1][kt][r] + bq[C + 32 * h + 16 + 4 * g + r];
+    }
+    pack8(x, kf[kt][0], kf[kt][1]);
+  }
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    const float bv = bq[2 * C + 32 * h + 16 * dt + j16];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float x[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        x[r] = av[2 * s][dt][r] + bv;
+        x[4 + r] = av[2 * s + 1][dt][r] + bv;
+      }
+      pack8(x, vf[dt][s][0], vf[dt][s][1]);
+    }
+  }
+  const float scale = 0.17677669529663687f;  // 32 ** -0.5
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {
+    float x[8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      x[r] = (aq[0][qt][r] + bq[32 * h + 4 * g + r]) * scale;
+      x[4 + r] = (aq[1][qt][r] + bq[32 * h + 16 + 4 * g + r]) * scale;
+    }
+    pack8(x, qf4[qt][0], qf4[qt][1]);
+  }
+
+  // ---- C
+  int type = 0;
+  if (wg.sh + wg.sw > 0) type = 2 * (wy == wg.nWin / wg.nWx - 1) + (wx == wg.nWx - 1);
+  attend_to_planes<X3, C>(kf, vf, qf4, p.table + ((size_t)type * HEADS + h) * 64 * 64, j16, g,
+                          (size_t)((long)b * wg.nWin + win) * kWinTok, 32 * h, p.att_hi, p.att_lo);
 }
 
 template <int C, int OCC>
@@ -737,7 +959,7 @@ void launch_c(const SwinAttnParams& p, hipStream_t s) {
 }  // namespace
 
 bool swin_attn_fused_supported(int C) { return C == 96 || C == 192; }
-bool swin_attn_noproj_supported(int C) { return C == 384; }
+bool swin_attn_noproj_supported(int C) { return C == 384 || C == 768; }
 
 void launch_swin_attn_fused(const SwinAttnParams& p, hipStream_t s) {
   if (p.B <= 0) return;
@@ -757,8 +979,17 @@ void launch_swin_attn_noproj(const SwinAttnParams& p, hipStream_t s) {
   if ((p.wqkv_lo == nullptr) != (p.att_lo == nullptr) || !p.att_hi)
     throw std::runtime_error("swin_attn_noproj: ATT planes must match the weight planes");
   if (p.heads * 32 != p.C) throw std::runtime_error("swin_attn: head dim must be 32");
-  if (p.C != 384) throw std::runtime_error("swin_attn_noproj: built for C = 384");
+  if (p.C != 384 && p.C != 768) throw std::runtime_error("swin_attn_noproj: built for C = 384, 768");
   const unsigned grid = (unsigned)((long)p.B * p.wg.nWin);
+  if (p.C == 768) {
+    // two workgroups per window, 12 heads (waves) each
+    if (p.wqkv_lo)
+      swin_attn_noproj_ks_kernel<768, 3, 3, 12, 1><<<2 * grid, 768, 0, s>>>(p);
+    else
+      swin_attn_noproj_ks_kernel<768, 1, 3, 12, 1><<<2 * grid, 768, 0, s>>>(p);
+    MOCR_HIP_CHECK(hipGetLastError());
+    return;
+  }
   // 12 waves (one head each, 3 per SIMD, 166 VGPRs) and k-steps unrolled by 2: 285 us per
   // s3 block at B=64, 384² vs 313 (8 waves over the 12 heads, 2 per SIMD), 302 (8 waves,
   // unroll 4), 318 (8 waves, no unroll)

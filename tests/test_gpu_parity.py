@@ -50,11 +50,12 @@ def test_encoder_stages_match_oracle(pkg, g384):
         assert e < 1e-4, f"features[{k}] rel err {e}"
 
 
-@pytest.mark.parametrize("variant", [(), ("unfused_attn",), ("unfused_attn", "unfused_mlp")])
+@pytest.mark.parametrize("variant", [(), ("unfused_attn",), ("unfused_attn", "unfused_mlp"), ("s4_fused_attn",)])
 def test_bf16x3_encoder_stages_match_oracle(pkg, golden, variant):
     """bf16x3 encoder stage by stage: the fused stage-1/2 attention half (wattn.hip) and
-    MLP half (mlp.hip), and the unfused kernels they replace (MOCR_VARIANT_* flags), all
-    within 1e-4 of the fp32 oracle.  384x384: the stage-1 map is 96x96, padded to 98
+    MLP half (mlp.hip), the stage-3 no-proj kernel, the stage-4 two-half kernel (off in
+    production), and the unfused kernels they replace (MOCR_VARIANT_* flags), all within
+    1e-4 of the fp32 oracle.  384x384: the stage-1 map is 96x96, padded to 98
     (zero tokens) and rolled by 3 on odd blocks."""
     g = golden("g384_b2_pert")
     m = g["meta"]
