@@ -2,7 +2,8 @@
 // output checksum, for fast iteration and PMC runs on the encoder GEMM shapes.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/gemm_bench.hip
 //        -L handwritten-math-ocr-api_amd/lib -lmathocr -Wl,-rpath,<repo>/handwritten-math-ocr-api_amd/lib
-// Run:   tools/gemm_bench M N K passes epi iters   (epi 0 store, 1 gelu, 2 resadd)
+// Run:   tools/gemm_bench M N K passes epi iters [data]   (epi 0 store, 1 gelu, 2 resadd;
+//        data 0: hi and lo planes U(+-0.05), 1: lo planes U(+-0.05/256) as real splits, 2: zeros)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -22,13 +23,13 @@ using namespace mocr;
     }                                                                   \
   } while (0)
 
-__global__ void fill_bf16(uint16_t* p, size_t n, uint32_t seed) {
+__global__ void fill_bf16(uint16_t* p, size_t n, uint32_t seed, float scale) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     uint32_t h = (uint32_t)i * 2654435761u ^ seed;
     h ^= h >> 13;
     h *= 0x5bd1e995u;
     h ^= h >> 15;
-    const float f = ((h & 0xffff) / 32768.0f - 1.0f) * 0.05f;  // uniform +-0.05
+    const float f = ((h & 0xffff) / 32768.0f - 1.0f) * scale;  // uniform +-scale
     p[i] = (uint16_t)(__float_as_uint(f) >> 16);
   }
 }
@@ -50,10 +51,12 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&Ch, (size_t)M * N * 2));
   CK(hipMalloc(&Cl, (size_t)M * N * 2));
   CK(hipMalloc(&bias, (size_t)N * 4));
-  fill_bf16<<<1024, 256>>>(A, (size_t)M * K, 1);
-  fill_bf16<<<1024, 256>>>(Al, (size_t)M * K, 2);
-  fill_bf16<<<1024, 256>>>(W, (size_t)N * K, 3);
-  fill_bf16<<<1024, 256>>>(Wl, (size_t)N * K, 4);
+  const int data = argc > 7 ? atoi(argv[7]) : 0;
+  const float hs = data == 2 ? 0.f : 0.05f, ls = data == 0 ? 0.05f : (data == 1 ? 0.05f / 256 : 0.f);
+  fill_bf16<<<1024, 256>>>(A, (size_t)M * K, 1, hs);
+  fill_bf16<<<1024, 256>>>(Al, (size_t)M * K, 2, ls);
+  fill_bf16<<<1024, 256>>>(W, (size_t)N * K, 3, hs);
+  fill_bf16<<<1024, 256>>>(Wl, (size_t)N * K, 4, ls);
   CK(hipMemset(C, 0, (size_t)M * N * 4));
   CK(hipMemset(bias, 0, (size_t)N * 4));
   GemmParams p{};
