@@ -16,6 +16,20 @@ constexpr int kWin = 7;        // Swin window
 constexpr int kWinTok = 49;    // tokens per window
 constexpr int kHeadDim = 32;   // Swin and decoder head dim (96/3 ... 768/24; 256/8)
 
+// A 16-B row slice the greedy decode streams once per step (cross-attention K/V, the
+// self-attention cache): a non-temporal load, so that the K/V streams do not evict the
+// decoder weights and activations that every step re-reads from L2 / the Infinity Cache.
+#ifndef MOCR_KV_NT
+#define MOCR_KV_NT 1
+#endif
+__device__ __forceinline__ floatx4 ld_stream4(const float* p) {
+#if MOCR_KV_NT
+  return __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(p));
+#else
+  return *reinterpret_cast<const floatx4*>(p);
+#endif
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

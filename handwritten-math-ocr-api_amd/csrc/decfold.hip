@@ -236,8 +236,8 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   for (int it = 0; it < NIT; ++it) {
     const int m = m_first + it * 4 * RPW;
     const size_t ml = (size_t)(m < n_cached ? m : 0);  // row 0 is allocated; masked below
-    kk[it] = *reinterpret_cast<const floatx4*>(Kb + ml * p.kv_row_stride);
-    vv[it] = *reinterpret_cast<const floatx4*>(Vb + ml * p.kv_row_stride);
+    kk[it] = ld_stream4(Kb + ml * p.kv_row_stride);
+    vv[it] = ld_stream4(Vb + ml * p.kv_row_stride);
   }
   constexpr int NP = SELF ? 3 : 1;  // q (| k | v)
   const float* zr = p.z + (size_t)b * p.z_ld + cc;

@@ -1493,6 +1493,7 @@ struct mocr_engine {
       }
     }
     MOCR_HIP_CHECK(hipMemcpyAsync(&hs, st, sizeof(hs), hipMemcpyDeviceToHost, stream));
+    MOCR_HIP_CHECK(hipStreamSynchronize(stream));  // hs is read below
     const int n = stop_batch && hs.done_step != 0x7fffffff ? hs.done_step + 1 : max_steps;
     if (timing) {
       // the whole graph-captured greedy decode as one record (launches = steps run)

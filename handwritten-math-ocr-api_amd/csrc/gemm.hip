@@ -780,6 +780,199 @@ __global__ void __launch_bounds__(512) gemm_bf16_stag_kernel(GemmParams p) {
   }
 }
 
+// ---------------------------------------------------------------- staggered kernel, whole rounds
+// gemm_bf16_stag_kernel's schedule (two wave groups one barrier apart, LOAD / COMPUTE
+// sections, counted DMA drains) for bf16x3 on BM x BN = 32 WTM x 64 WTN tiles: waves as
+// 2 (rows) x 4 (cols), each owning WTM x WTN MFMA tiles of 16 x 16, computed in phases of
+// PM x PN tiles visited in serpentine order, so a phase reloads only the A or only the W
+// fragments.  The shapes are picked so the tile count fills whole rounds of the 256 CUs on
+// the stage-3 GEMMs (M = 576 B, a multiple of 288): 288 x 256 on s3.fc1 is 768 tiles =
+// 3 rounds (256 x 256: 864 tiles, a 4th round 38 % full), 288 x 192 on s3.fc2 / s3.proj
+// 256 tiles = 1 round (128 x 128: 864 tiles).  Per output element the MFMA sequence is the
+// other kernels' (hi·hi, hi·lo, lo·hi per 32-deep k-tile, k ascending), so the results
+// are bitwise equal to theirs.
+template <int EPI, int WTM, int WTN, int PM, int PN>
+__global__ void __launch_bounds__(512) gemm_x3_stagq_kernel(GemmParams p) {
+  constexpr int BM = 32 * WTM, BN = 64 * WTN;
+  constexpr int KT = 32, ROWB = 128;  // one LDS row: 32 k of the hi plane | 32 k of the lo plane
+  constexpr int A_B = BM * ROWB;
+  constexpr int BUF = (BM + BN) * ROWB;
+  constexpr int NPM = WTM / PM, NPN = WTN / PN, NPH = NPM * NPN;
+  static_assert(NPM * PM == WTM && NPN * PN == WTN && NPH >= 2, "phase split");
+  static_assert(BM % 16 == 0, "the W rows keep the A rows' swizzle phase");
+  constexpr int PIECES = (BM + BN) / 8;   // one glds = 8 rows x 128 B
+  constexpr int PPW = (PIECES + 7) / 8;   // per wave; spare slots repeat the last piece
+  constexpr int PPH0 = (PPW + 1) / 2;     // issued in phase 0, the rest in phase 1
+  constexpr int CR = WTM % 3 == 0 ? 3 : 2;  // epilogue: CR row tiles per slab round
+  static_assert(WTM % CR == 0, "epilogue rounds");
+  constexpr int EW = 16 * WTN, ES = EW + 4, ER = 16 * CR;
+  constexpr int EV = ER * EW / 8;  // 8-float vectors per slab round per wave
+  static_assert(8 * ER * ES * 4 <= 2 * BUF, "epilogue slab");
+  __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave >> 2;
+  const int wc = wave & 3;
+  int tx, ty;
+  tile_of(p.N / BN, tx, ty);
+  const int row0 = ty * BM;
+  const int col0 = tx * BN;
+  const int nk = p.K / KT;
+  const char* A0 = static_cast<const char*>(p.A);
+  const char* A1 = static_cast<const char*>(p.A_lo);
+  const char* W0 = static_cast<const char*>(p.W);
+  const char* W1 = static_cast<const char*>(p.W_lo);
+
+  // DMA piece pc = rows 8 pc .. 8 pc + 7 of the [A | W] image; lane: row + lane / 8,
+  // LDS chunk lane % 8, which holds global chunk (lane % 8) ^ swz8(row)
+  const int drow = lane >> 3;
+  const int dch = lane & 7;
+  const int lda = p.lda, ldw = p.ldw, M = p.M;
+  // lo-plane offsets as integers: a select between two captured pointers put them in scratch
+  const ptrdiff_t dA = A1 - A0, dW = W1 - W0;
+  auto issue1 = [&](int kt, int i) {  // this wave's piece i of K-tile kt
+    char* buf = lds + (kt & 1) * BUF;
+    const int k0 = kt * KT;
+    {
+      const int pc = min(wave * PPW + i, PIECES - 1);
+      const int r = pc * 8 + drow;
+      const int sc = dch ^ swz8(r);
+      const char* src;
+      if (pc < BM / 8) {
+        const size_t gr = (size_t)min(row0 + r, M - 1);
+        src = A0 + (sc < 4 ? 0 : dA) + (gr * lda + k0 + 8 * (sc & 3)) * 2;
+      } else {
+        const size_t gr = (size_t)(col0 + r - BM);
+        src = W0 + (sc < 4 ? 0 : dW) + (gr * ldw + k0 + 8 * (sc & 3)) * 2;
+      }
+      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(buf + pc * 8 * ROWB), 16, 0, 0);
+    }
+  };
+
+  floatx4 acc[WTM][WTN];
+#pragma unroll
+  for (int i = 0; i < WTM; ++i)
+#pragma unroll
+    for (int j = 0; j < WTN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int l16 = lane & 15;
+  const int kq = lane >> 4;
+  bf16x8 fa[PM][2], fb[PN][2];  // [tile][plane: 0 hi, 1 lo]
+  auto load_a = [&](const char* buf, int qm) {
+#pragma unroll
+    for (int i = 0; i < PM; ++i) {
+      const int r = wr * (BM / 2) + (qm * PM + i) * 16 + l16;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        fa[i][s2] = *reinterpret_cast<const bf16x8*>(buf + r * ROWB + 16 * ((4 * s2 + kq) ^ swz8(r)));
+    }
+  };
+  auto load_b = [&](const char* buf, int qn) {
+#pragma unroll
+    for (int j = 0; j < PN; ++j) {
+      const int r = wc * EW + (qn * PN + j) * 16 + l16;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        fb[j][s2] = *reinterpret_cast<const bf16x8*>(buf + A_B + r * ROWB + 16 * ((4 * s2 + kq) ^ swz8(r)));
+    }
+  };
+
+  // prologue: K-tile 0 into buffer 0, visible to all; group 1 then falls one barrier behind
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) issue1(0, i);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* buf = lds + (kt & 1) * BUF;
+    const bool more = kt + 1 < nk;
+#pragma unroll
+    for (int ph = 0; ph < NPH; ++ph) {
+      const int qm = ph / NPN;
+      const int qn = (qm & 1) ? NPN - 1 - ph % NPN : ph % NPN;  // serpentine
+      // LOAD
+      if (ph == 0) {
+        load_b(buf, qn);
+        load_a(buf, qm);
+      } else if (ph % NPN == 0) {
+        load_a(buf, qm);
+      } else {
+        load_b(buf, qn);
+      }
+      if (more) {
+        if (ph == 0)
+#pragma unroll
+          for (int i = 0; i < PPH0; ++i) issue1(kt + 1, i);
+        if (ph == 1)
+#pragma unroll
+          for (int i = PPH0; i < PPW; ++i) issue1(kt + 1, i);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (ph == NPH - 1 && wr == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      // COMPUTE
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < PM; ++i)
+#pragma unroll
+        for (int j = 0; j < PN; ++j) {
+          floatx4& c = acc[qm * PM + i][qn * PN + j];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
+        }
+      __builtin_amdgcn_s_setprio(0);
+      if (ph == NPH - 1 && wr == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // pair group 1's extra barrier
+  __builtin_amdgcn_s_barrier();
+
+  // epilogue: per-wave LDS transpose, ER rows x EW columns per round
+  float* ep = reinterpret_cast<float*>(lds) + wave * ER * ES;
+#pragma unroll
+  for (int h = 0; h < WTM / CR; ++h) {
+#pragma unroll
+    for (int i2 = 0; i2 < CR; ++i2)
+#pragma unroll
+      for (int j = 0; j < WTN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ep[(i2 * 16 + 4 * kq + r) * ES + j * 16 + l16] = acc[h * CR + i2][j][r];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int it = 0; it < (EV + 63) / 64; ++it) {
+      const int idx = it * 64 + lane;
+      if (EV % 64 == 0 || idx < EV) {
+        const int rr = idx / (EW / 8);
+        const int cc = idx - rr * (EW / 8);
+        const floatx4 v0 = *reinterpret_cast<const floatx4*>(ep + rr * ES + cc * 8);
+        const floatx4 v1 = *reinterpret_cast<const floatx4*>(ep + rr * ES + cc * 8 + 4);
+        float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        const int row = row0 + wr * (BM / 2) + h * ER + rr;
+        if (row < M) epi_vec8<EPI>(p, row, col0 + wc * EW + cc * 8, v);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+template <int WTM, int WTN, int PM, int PN>
+void launch_stagq(const GemmParams& p, hipStream_t s) {
+  constexpr int BM = 32 * WTM, BN = 64 * WTN;
+  const dim3 grid((unsigned)((p.N / BN) * ((p.M + BM - 1) / BM)));
+  switch (p.epi) {
+    case EPI_STORE: gemm_x3_stagq_kernel<EPI_STORE, WTM, WTN, PM, PN><<<grid, 512, 0, s>>>(p); break;
+    case EPI_GELU: gemm_x3_stagq_kernel<EPI_GELU, WTM, WTN, PM, PN><<<grid, 512, 0, s>>>(p); break;
+    case EPI_RESADD: gemm_x3_stagq_kernel<EPI_RESADD, WTM, WTN, PM, PN><<<grid, 512, 0, s>>>(p); break;
+    case EPI_WINRES: gemm_x3_stagq_kernel<EPI_WINRES, WTM, WTN, PM, PN><<<grid, 512, 0, s>>>(p); break;
+    default: throw std::runtime_error("gemm_bf16: bad epilogue");
+  }
+}
+
 // Staggered 256 x 256 kernel: measured (B=64, 384²) faster than the ring kernels on bf16x3
 // GEMMs with K <= N and at least 384 tiles (s3.fc1 225 -> 217 us, s4.fc1 163 -> 154),
 // slower with K > N or fewer tiles and in plain bf16.
@@ -836,8 +1029,62 @@ bool try_big_tile(const GemmParams& p, hipStream_t s) {
   return true;
 }
 
+// force_kernel values (tools/gemm_bench A/B; 0 = the dispatch's choice)
+enum : int { kKernelAuto = -1, kKernelStag = 1, kKernelBig = 2, kKernelTile = 3, kKernelQ288x256 = 10, kKernelQ288x192 = 11 };
+
+template <int PASSES>
+void launch_forced(const GemmParams& p, hipStream_t s) {
+  const bool x3 = PASSES == 3;
+  switch (p.force_kernel) {
+    case kKernelAuto:  // the dispatch before the 288-row tiles
+      if (try_stag<PASSES>(p, s) || try_big_tile<PASSES>(p, s)) return;
+      if (p.N % 128 == 0) return launch_tile16<4, 4, 2, 2, PASSES, 2>(p, s);
+      if (p.N % 96 == 0) return launch_tile16<4, 3, 2, 2, PASSES, 2>(p, s);
+      break;
+    case kKernelStag:
+      if (try_stag<PASSES>(p, s)) return;
+      break;
+    case kKernelBig:
+      if (try_big_tile<PASSES>(p, s)) return;
+      break;
+    case kKernelTile:
+      if (p.N % 128 == 0) return launch_tile16<4, 4, 2, 2, PASSES, 2>(p, s);
+      if (p.N % 96 == 0) return launch_tile16<4, 3, 2, 2, PASSES, 2>(p, s);
+      break;
+    case kKernelQ288x256:
+      if (x3 && p.N % 256 == 0) return launch_stagq<9, 4, 3, 2>(p, s);
+      break;
+    case kKernelQ288x192:
+      if (x3 && p.N % 192 == 0) return launch_stagq<9, 3, 3, 3>(p, s);
+      break;
+  }
+  throw std::runtime_error("gemm_bf16: forced kernel does not fit the shape");
+}
+
+// 288-row staggered tiles where they fill whole rounds of the 256 CUs (bf16x3; measured
+// on the stage-3 shapes, tools/gemm_bench: s3.fc2 175 -> 143 us, s3.proj 52 -> 46,
+// s3.fc1 194 -> 183; equal on s4.fc1; slower than the 256 x 256 / ring kernels on the
+// stage-4 shapes that leave a partial round, which keep those)
+template <int PASSES>
+bool try_stagq(const GemmParams& p, hipStream_t s) {
+  if (PASSES != 3) return false;
+  const long mt = (p.M + 287) / 288;
+  auto whole = [](long tiles) { return tiles >= 256 && tiles % 256 == 0; };
+  if (p.K <= p.N && p.N % 256 == 0 && whole(mt * (p.N / 256))) {
+    launch_stagq<9, 4, 3, 2>(p, s);
+    return true;
+  }
+  if (p.N % 192 == 0 && whole(mt * (p.N / 192))) {
+    launch_stagq<9, 3, 3, 3>(p, s);
+    return true;
+  }
+  return false;
+}
+
 template <int PASSES>
 void launch_bf16_passes(const GemmParams& p, hipStream_t s) {
+  if (p.force_kernel) return launch_forced<PASSES>(p, s);
+  if (try_stagq<PASSES>(p, s)) return;
   if (try_stag<PASSES>(p, s)) return;
   if (try_big_tile<PASSES>(p, s)) return;
   if (p.N % 128 == 0) {  // 128 x 128, waves of 64 x 64

@@ -54,6 +54,7 @@ struct GemmParams {
   size_t split_stride; // floats between column blocks: C[col/cs][row][col%cs]
   ConvGeom conv;       // conv.on: A is the implicit im2col of an NHWC map (bf16 planes)
   const void* zero;    // >= 64 zero bytes (conv padding taps)
+  int force_kernel;    // 0: the dispatch's choice; tools/gemm_bench A/B: launch_gemm_bf16 kKernel*
 };
 
 void launch_gemm_f32(const GemmParams& p, hipStream_t s);

@@ -2,8 +2,9 @@
 // output checksum, for fast iteration and PMC runs on the encoder GEMM shapes.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/gemm_bench.hip
 //        -L handwritten-math-ocr-api_amd/lib -lmathocr -Wl,-rpath,<repo>/handwritten-math-ocr-api_amd/lib
-// Run:   tools/gemm_bench M N K passes epi iters [data]   (epi 0 store, 1 gelu, 2 resadd;
-//        data 0: hi and lo planes U(+-0.05), 1: lo planes U(+-0.05/256) as real splits, 2: zeros)
+// Run:   tools/gemm_bench M N K passes epi iters [data [kernel]]   (epi 0 store, 1 gelu, 2 resadd;
+//        data 0: hi and lo planes U(+-0.05), 1: lo planes U(+-0.05/256) as real splits, 2: zeros;
+//        kernel: GemmParams::force_kernel, 0 = the dispatch's choice)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -72,6 +73,7 @@ int main(int argc, char** argv) {
   p.ldw = K;
   p.ldc = N;
   p.epi = epi;
+  p.force_kernel = argc > 8 ? atoi(argv[8]) : 0;
   if (epi == EPI_RESADD) {
     p.C = C;
   } else {
