@@ -17,6 +17,7 @@
 // address and are masked after the load (hipcc turns `c ? *p : 0` into a branch and a
 // full vmcnt(0) wait per element).
 #include "kernels.h"
+#include "select.h"
 
 namespace mocr {
 
@@ -209,7 +210,11 @@ __global__ void __launch_bounds__(64 * NW) foldgemm_kernel(FoldGemmParams p) {
 // Each lane unfolds its 4 columns of q -- and, self-attention, of the new k and v --
 // from z; the lanes of key slot t take the new k/v from registers, and wave 0's first
 // key group appends them to the cache.  ZS: z carries statistics (else z is final).
-template <bool SELF, bool ZS, int NIT>
+// SEL (layer 0 of steps t >= 1): the workgroup first runs the greedy selection of step
+// t-1 for its row (select.h; the head-0 workgroup does the bookkeeping), then takes q|k|v
+// of the selected token from the tables and writes its 32 columns of x = emb + pos --
+// the work of a separate argmax kernel at the end of step t-1, without its launch.
+template <bool SELF, bool ZS, bool SEL, int NIT>
 __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   constexpr int LPR = 8;  // lanes per key row
   constexpr int RPW = 8;  // key rows per wave instruction
@@ -240,14 +245,33 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
     vv[it] = ld_stream4(Vb + ml * p.kv_row_stride);
   }
   constexpr int NP = SELF ? 3 : 1;  // q (| k | v)
-  const float* zr = p.z + (size_t)b * p.z_ld + cc;
   floatx4 zv[NP], sv[NP], cv[NP];
+  if constexpr (SEL) {
+    static_assert(SELF && !ZS, "selection runs in layer 0's self-attention");
+    const int tok = greedy_select(p.sel, b, h == 0);
+    const int tk = max(tok, 0);  // -1: the batch stopped before step t-1 (nothing is written)
+    const float* qt = p.qtab + (size_t)tk * 3 * kD + cc;
+    const float* qp = p.qpos + (size_t)t * 3 * kD + cc;
 #pragma unroll
-  for (int j = 0; j < NP; ++j) {
-    zv[j] = *reinterpret_cast<const floatx4*>(zr + j * kD);
-    if constexpr (ZS) {
-      sv[j] = *reinterpret_cast<const floatx4*>(p.s + j * kD + cc);
-      cv[j] = *reinterpret_cast<const floatx4*>(p.c + j * kD + cc);
+    for (int j = 0; j < NP; ++j) {
+      const floatx4 a4 = *reinterpret_cast<const floatx4*>(qt + j * kD);
+      const floatx4 b4 = *reinterpret_cast<const floatx4*>(qp + j * kD);
+      zv[j] = a4 + b4;
+    }
+    if (tok >= 0 && wave == 0 && rsub == 0) {
+      const floatx4 e4 = *reinterpret_cast<const floatx4*>(p.emb + (size_t)tk * kD + cc);
+      const floatx4 p4 = *reinterpret_cast<const floatx4*>(p.pos + (size_t)t * kD + cc);
+      *reinterpret_cast<floatx4*>(p.x + (size_t)b * kD + cc) = e4 + p4;
+    }
+  } else {
+    const float* zr = p.z + (size_t)b * p.z_ld + cc;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      zv[j] = *reinterpret_cast<const floatx4*>(zr + j * kD);
+      if constexpr (ZS) {
+        sv[j] = *reinterpret_cast<const floatx4*>(p.s + j * kD + cc);
+        cv[j] = *reinterpret_cast<const floatx4*>(p.c + j * kD + cc);
+      }
     }
   }
   if constexpr (ZS) {
@@ -395,19 +419,24 @@ void launch_dec_foldattn(const FoldAttnParams& p, bool self_attn, hipStream_t s)
   if (zs && (!p.s || !p.c)) throw std::runtime_error("foldattn: statistics need s and c");
   if (self_attn && (!p.kcache || !p.vcache || p.n != p.t + 1 || p.z_ld < 3 * kD))
     throw std::runtime_error("foldattn: self-attention needs the cache, n = t + 1 and q|k|v");
+  if (p.sel_on && (!self_attn || zs || !p.qtab || !p.qpos || !p.emb || !p.pos || !p.x || p.sel.t != p.t - 1 ||
+                   (p.sel.part && p.sel.nparts > 512)))
+    throw std::runtime_error("foldattn: the selection runs in layer 0's self-attention of step sel.t + 1");
   if (p.B <= 0) return;
   const int nit = (p.n + 31) / 32;  // 32 key rows per workgroup pass (4 waves x 8 rows)
   const dim3 grid(p.B, kD / 32);
 #define MOCR_FA(N)                                                                    \
   case N:                                                                             \
     if (self_attn && zs)                                                              \
-      dec_foldattn_kernel<true, true, N><<<grid, 256, 0, s>>>(p);                     \
+      dec_foldattn_kernel<true, true, false, N><<<grid, 256, 0, s>>>(p);              \
+    else if (self_attn && p.sel_on)                                                   \
+      dec_foldattn_kernel<true, false, true, N><<<grid, 256, 0, s>>>(p);              \
     else if (self_attn)                                                               \
-      dec_foldattn_kernel<true, false, N><<<grid, 256, 0, s>>>(p);                    \
+      dec_foldattn_kernel<true, false, false, N><<<grid, 256, 0, s>>>(p);             \
     else if (zs)                                                                      \
-      dec_foldattn_kernel<false, true, N><<<grid, 256, 0, s>>>(p);                    \
+      dec_foldattn_kernel<false, true, false, N><<<grid, 256, 0, s>>>(p);             \
     else                                                                              \
-      dec_foldattn_kernel<false, false, N><<<grid, 256, 0, s>>>(p);                   \
+      dec_foldattn_kernel<false, false, false, N><<<grid, 256, 0, s>>>(p);            \
     break;
   switch (nit) {
     MOCR_FA(1) MOCR_FA(2) MOCR_FA(3) MOCR_FA(4) MOCR_FA(5) MOCR_FA(6) MOCR_FA(7) MOCR_FA(8) MOCR_FA(9)

@@ -19,6 +19,7 @@
 // no kernel reads device state before issuing its loads.  With the batch-global stop,
 // the stop flag is read alongside the loads and checked before the first store.
 #include "kernels.h"
+#include "select.h"
 
 namespace mocr {
 
@@ -772,123 +773,23 @@ __global__ void __launch_bounds__(256) ln_rows_kernel(const float* __restrict__ 
 }
 
 // ------------------------------------------------------------------ greedy select
-// argmax over the vocabulary (first maximal index, as torch.argmax), log-prob of the
-// chosen token log(softmax + 1e-10) (app/src/im2latex.py:33-39), EOS bookkeeping for
-// the batch-global stop (src/inference.py:23-25), and the embedding of the token fed
-// to step t+1.
-__global__ void __launch_bounds__(256) dec_argmax_kernel(DecodeState* st, int t, int last_step,
-                                                         const float* __restrict__ logits, size_t hist_stride, int ldl,
-                                                         int V,
-                                                         int32_t* __restrict__ ids, int32_t* __restrict__ feed,
-                                                         const int32_t* __restrict__ forced, int ld_ids,
-                                                         float* __restrict__ logp, int32_t* __restrict__ finished,
-                                                         int eos, int stop_batch, const float* __restrict__ emb,
+// select.h greedy_select for step t (one workgroup per row), then the embedding of the
+// token fed to step t+1 (and, folded step, layer 0's q|k|v of it).  The folded step runs
+// the selection of steps 0 .. n-2 inside the next step's layer-0 self-attention
+// (decfold.hip), so this kernel only ends the last step there.
+__global__ void __launch_bounds__(256) dec_argmax_kernel(SelectArgs a, int last_step, const float* __restrict__ emb,
                                                          const float* __restrict__ pos, float* __restrict__ x,
                                                          int d, const float* __restrict__ qtab,
-                                                         const float* __restrict__ qpos, float* __restrict__ z,
-                                                         const float* __restrict__ part, int nparts) {
+                                                         const float* __restrict__ qpos, float* __restrict__ z) {
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const float* L = logits + (hist_stride ? (size_t)t * hist_stride : 0) + (size_t)b * ldl;
-  // one pass: running (max, first argmax, Σ exp(l - max)) per thread, then merged
-  float best = -INFINITY, sum = 0.f;
-  int bidx = 0x7fffffff;
-  auto merge = [](float& b1, int& i1, float& s1, float b2, int i2, float s2) {
-    const float m = fmaxf(b1, b2);
-    const float f1 = b1 == -INFINITY ? 0.f : expf(b1 - m);
-    const float f2 = b2 == -INFINITY ? 0.f : expf(b2 - m);
-    s1 = s1 * f1 + s2 * f2;
-    if (b2 > b1 || (b2 == b1 && i2 < i1)) i1 = i2;
-    b1 = m;
-  };
-  constexpr int CH = 20;  // loads in flight per thread: one round for V <= 5120
-  if (part) {  // per-16-column-tile partials of the logits kernel: 2 per thread for V <= 8192
-    const floatx4* P = reinterpret_cast<const floatx4*>(part) + (size_t)b * nparts;
-    floatx4 q[2];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) q[c] = P[min(tid + 256 * c, nparts - 1)];
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-      if (tid + 256 * c < nparts) merge(best, bidx, sum, q[c][0], __float_as_int(q[c][1]), q[c][2]);
-  }
-  for (int j0 = part ? V : tid; j0 < V; j0 += 256 * CH) {
-    float vals[CH];
-    // unpredicated loads (a clamped column), masked after: a predicated load per element
-    // becomes a branch + vmcnt(0) each
-#pragma unroll
-    for (int c = 0; c < CH; ++c) vals[c] = L[min(j0 + 256 * c, V - 1)];
-#pragma unroll
-    for (int c = 0; c < CH; ++c) vals[c] = (j0 + 256 * c < V) ? vals[c] : -INFINITY;
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const float v = vals[c];
-      if (v > best) {
-        sum = sum * expf(best - v) + 1.0f;
-        best = v;
-        bidx = j0 + 256 * c;
-      } else if (v != -INFINITY) {
-        sum += expf(v - best);
-      }
-    }
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ob = __shfl_xor(best, o, 64);
-    const int oi = __shfl_xor(bidx, o, 64);
-    const float os = __shfl_xor(sum, o, 64);
-    merge(best, bidx, sum, ob, oi, os);
-  }
-  __shared__ float sv[4], ss[4];
-  __shared__ int si_[4];
-  __shared__ int s_next;
-  if (lane == 0) {
-    sv[wave] = best;
-    si_[wave] = bidx;
-    ss[wave] = sum;
-  }
-  __syncthreads();
-  best = sv[0];
-  bidx = si_[0];
-  sum = ss[0];
-#pragma unroll
-  for (int w = 1; w < 4; ++w) merge(best, bidx, sum, sv[w], si_[w], ss[w]);
-  if (dec_skip(stop_batch ? st : nullptr, t)) return;
-  // A row without a finite maximum (NaN logits never win `v > best`) would leave bidx at
-  // INT_MAX and gather the next embedding ~2^31 rows out of bounds: clamp it to a valid
-  // id and count the row; the host turns the count into an error after the decode.
-  if (!(bidx >= 0 && bidx < V && isfinite(best) && sum > 0.f)) {
-    if (tid == 0) atomicAdd(&st->bad_rows, 1);
-    bidx = 0;
-    sum = 1.f;
-  }
-  if (tid == 0) {
-    int next = forced ? forced[(size_t)b * ld_ids + t + 1] : bidx;
-    next = min(max(next, 0), V - 1);
-    ids[(size_t)b * ld_ids + t + 1] = bidx;
-    feed[(size_t)b * ld_ids + t + 1] = next;
-    logp[(size_t)b * (ld_ids - 1) + t] = logf(1.0f / sum + 1e-10f);
-    s_next = next;
-    if (bidx == eos && !finished[b]) {
-      finished[b] = 1;
-      atomicMax(&st->last_finish, t);
-      __threadfence();
-      const int before = atomicAdd(&st->nfinished, 1);
-      if (before == st->batch - 1 && stop_batch) {
-        __threadfence();
-        st->done_step = atomicMax(&st->last_finish, t);
-      }
-    }
-  }
-  __syncthreads();
-  if (!last_step) {
-    const int tok = s_next;
-    for (int c = tid; c < d; c += 256) x[(size_t)b * d + c] = emb[(size_t)tok * d + c] + pos[(size_t)(t + 1) * d + c];
-    if (qtab)  // folded step: layer 0's q|k|v of the fed token at position t+1
-      for (int c = tid; c < 3 * d; c += 256)
-        z[(size_t)b * 3 * d + c] = qtab[(size_t)tok * 3 * d + c] + qpos[(size_t)(t + 1) * 3 * d + c];
-  }
+  const int t = a.t;
+  const int tok = greedy_select(a, b, true);
+  if (tok < 0 || last_step) return;
+  for (int c = tid; c < d; c += 256) x[(size_t)b * d + c] = emb[(size_t)tok * d + c] + pos[(size_t)(t + 1) * d + c];
+  if (qtab)  // folded step: layer 0's q|k|v of the fed token at position t+1
+    for (int c = tid; c < 3 * d; c += 256)
+      z[(size_t)b * 3 * d + c] = qtab[(size_t)tok * 3 * d + c] + qpos[(size_t)(t + 1) * 3 * d + c];
 }
 
 }  // namespace
@@ -939,14 +840,10 @@ void launch_dec_attn(const DecodeState* st, int t, const float* q, const float* 
   MOCR_HIP_CHECK(hipGetLastError());
 }
 
-void launch_dec_argmax(DecodeState* st, int t, int last_step, const float* logits, size_t hist_stride, int ldl,
-                       int V, int B, int32_t* ids, int32_t* feed, const int32_t* forced, int ld_ids, float* logp,
-                       int32_t* finished, int eos, int stop_batch, const float* emb, const float* pos, float* x,
-                       int d, hipStream_t s, const float* qtab, const float* qpos, float* z, const float* part) {
-  const int nparts = ldl / 16;
-  if (part && nparts > 512) throw std::runtime_error("argmax: at most 8192 logits with tile partials");
-  dec_argmax_kernel<<<B, 256, 0, s>>>(st, t, last_step, logits, hist_stride, ldl, V, ids, feed, forced, ld_ids, logp,
-                                      finished, eos, stop_batch, emb, pos, x, d, qtab, qpos, z, part, nparts);
+void launch_dec_argmax(const SelectArgs& a, int last_step, int B, const float* emb, const float* pos, float* x, int d,
+                       hipStream_t s, const float* qtab, const float* qpos, float* z) {
+  if (a.part && a.nparts > 512) throw std::runtime_error("argmax: at most 8192 logits with tile partials");
+  dec_argmax_kernel<<<B, 256, 0, s>>>(a, last_step, emb, pos, x, d, qtab, qpos, z);
   MOCR_HIP_CHECK(hipGetLastError());
 }
 

@@ -317,6 +317,7 @@ struct mocr_engine {
   float* logp = nullptr;
   DecodeState* st = nullptr;
   int ld_ids = 0;
+  const SelectArgs* sel_prev = nullptr;  // record_step -> record_layers_fold (layer 0 of step t >= 1)
   int max_rows = 0;  // decoder rows the buffers hold: max_batch * max(1, max_beam)
   // beam search: scores, finished flags, token sequences and K/V slot tables [2 parities]
   float* bscore = nullptr;
@@ -1296,6 +1297,10 @@ struct mocr_engine {
       FoldAttnParams a{};
       a.st = stp; a.t = t; a.B = B; a.out = datt; a.z = dzqkv; a.z_ld = 3 * d;
       if (l) { a.z_stats = ds_ff; a.s = foldw[l - 1].sqkv; a.c = foldw[l - 1].cqkv; }
+      if (!l && sel_prev) {  // step t-1's greedy selection, then q|k|v from the tables
+        a.sel_on = 1; a.sel = *sel_prev; a.qtab = qtab; a.qpos = qpos; a.emb = W(lay->emb); a.pos = W(lay->pos);
+        a.x = dx;
+      }
       a.K = kc; a.V = vc; a.kcache = kc; a.vcache = vc;
       a.kv_b_stride = (size_t)cfg.max_pos * d; a.kv_row_stride = d; a.n = t + 1;
       launch_dec_foldattn(a, true, s);
@@ -1356,17 +1361,41 @@ struct mocr_engine {
     launch_rowgemm(p, stream);
   }
 
+  // greedy selection of step t (select.h) over the logits slot record_logits writes
+  SelectArgs select_args(int t, bool hist, bool use_forced, bool stop_batch) const {
+    SelectArgs a{};
+    a.st = st; a.t = t; a.logits = hist ? dlogits_hist : dlogits; a.hist_stride = hist ? (size_t)cfg.max_batch * Vpad : 0;
+    a.ldl = Vpad; a.V = cfg.vocab; a.ids = ids; a.feed = feed; a.forced = use_forced ? forced : nullptr;
+    a.ld_ids = ld_ids; a.logp = logp; a.finished = finished; a.eos = cfg.eos_id; a.stop_batch = stop_batch ? 1 : 0;
+    a.part = dpart; a.nparts = Vpad / 16;
+    return a;
+  }
+
+  // The folded step runs step t-1's selection in step t's first kernel (layer 0's
+  // self-attention, decfold.hip): 41 dependent launches per step; only the last step
+  // ends with dec_argmax_kernel.
   void record_step(int B, int t, int max_steps, bool hist, bool use_forced, bool stop_batch) {
     const DecodeState* stp = stop_batch ? st : nullptr;
-    record_layers(B, t, stp, nullptr, 1);
+    const bool fold = fold_greedy();
+    SelectArgs prev{};
+    if (fold && t > 0) {
+      prev = select_args(t - 1, hist, use_forced, stop_batch);
+      sel_prev = &prev;
+    }
+    try {
+      record_layers(B, t, stp, nullptr, 1);
+    } catch (...) {
+      sel_prev = nullptr;
+      throw;
+    }
+    sel_prev = nullptr;
     float* out = hist ? dlogits_hist : dlogits;
     const size_t hs = hist ? (size_t)cfg.max_batch * Vpad : 0;
     record_logits(B, t, stp, out, hs, dpart);
-    const bool fold = fold_greedy();
-    launch_dec_argmax(st, t, t + 1 >= max_steps, out, hs, Vpad, cfg.vocab, B, ids, feed, use_forced ? forced : nullptr,
-                      ld_ids, logp, finished, cfg.eos_id, stop_batch ? 1 : 0, W(lay->emb), W(lay->pos), dx,
-                      cfg.d_model, stream, fold ? qtab : nullptr, fold ? qpos : nullptr, fold ? dzqkv : nullptr,
-                      dpart);
+    if (!fold || t + 1 >= max_steps)
+      launch_dec_argmax(select_args(t, hist, use_forced, stop_batch), t + 1 >= max_steps, B, W(lay->emb), W(lay->pos),
+                        dx, cfg.d_model, stream, fold ? qtab : nullptr, fold ? qpos : nullptr,
+                        fold ? dzqkv : nullptr);
   }
 
   BeamParams beam_params(int B, int K, int t, int max_steps, bool stop_batch) {

@@ -202,6 +202,25 @@ void launch_foldgemm(const FoldGemmParams& p, hipStream_t s);
 // q = rstd (z_q - mu s) + c from z [B, z_ld] and z_stats (plain z when z_stats is null).
 // Self-attention: z holds q|k|v (s, c: [3d]); the new k/v are appended to the cache at t
 // and the keys are cache rows 0..t.  Cross-attention: K/V = the memory K/V, n = M.
+// Greedy selection of step t (select.h): logits (or the logits kernel's per-16-column
+// (max, first argmax, sum exp) partials, nparts per row) -> ids / feed / logp, finished
+// flags and the batch-global stop state.
+struct SelectArgs {
+  DecodeState* st;
+  int t;
+  const float* logits;
+  size_t hist_stride;  // logits of step t at logits + t * hist_stride (0: one slot)
+  int ldl, V;
+  int32_t *ids, *feed;
+  const int32_t* forced;  // teacher forcing (parity tests), or null
+  int ld_ids;
+  float* logp;
+  int32_t* finished;
+  int eos, stop_batch;
+  const float* part;
+  int nparts;
+};
+
 struct FoldAttnParams {
   const DecodeState* st;
   int t;
@@ -216,6 +235,12 @@ struct FoldAttnParams {
   int n;                   // keys (self: t + 1)
   float* out;              // [B, d]
   int B;
+  // layer 0 of step t >= 1: the greedy selection of step t-1 runs here (sel.t = t - 1),
+  // q|k|v of the selected token come from the tables, x = emb + pos is written
+  int sel_on;
+  SelectArgs sel;
+  const float *qtab, *qpos, *emb, *pos;
+  float* x;
 };
 void launch_dec_foldattn(const FoldAttnParams& p, bool self_attn, hipStream_t s);
 
@@ -294,10 +319,7 @@ void launch_dec_attn(const DecodeState* st, int t, const float* q, const float* 
 
 // Argmax + log-prob + finish flags + next fed token + next step's embedding.  With `part`
 // (the logits kernel's tile partials [B][ldl/16] float4) the logits are not re-read.
-void launch_dec_argmax(DecodeState* st, int t, int last_step, const float* logits, size_t hist_stride, int ldl,
-                       int V, int B, int32_t* ids, int32_t* feed, const int32_t* forced, int ld_ids, float* logp,
-                       int32_t* finished, int eos, int stop_batch, const float* emb, const float* pos, float* x,
-                       int d, hipStream_t s, const float* qtab = nullptr, const float* qpos = nullptr,
-                       float* z = nullptr, const float* part = nullptr);
+void launch_dec_argmax(const SelectArgs& a, int last_step, int B, const float* emb, const float* pos, float* x, int d,
+                       hipStream_t s, const float* qtab = nullptr, const float* qpos = nullptr, float* z = nullptr);
 
 }  // namespace mocr

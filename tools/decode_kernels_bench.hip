@@ -81,6 +81,12 @@ int main(int argc, char** argv) {
       launch_foldgemm(p, ss);
     };
   };
+  auto sel = [=](const float* pt) {
+    SelectArgs a{};
+    a.st = st; a.t = t; a.logits = logits; a.ldl = Vp; a.V = V; a.ids = ids; a.feed = feed; a.ld_ids = 151;
+    a.logp = logp; a.finished = fin; a.eos = 2; a.part = pt; a.nparts = Vp / 16;
+    return a;
+  };
   std::vector<std::pair<std::string, std::function<void(hipStream_t)>>> cases = {
       {"qkv N768 K256 +LN(A)", rg(DEC_QKV, 768, 256, true, false)},
       {"oproj N256 K256 +LN(res)", rg(DEC_RESADD, 256, 256, false, true)},
@@ -96,7 +102,7 @@ int main(int argc, char** argv) {
          launch_dec_attn(nullptr, t, q, memkv, memkv + d, (size_t)M * 2 * d, 2 * d, M, M, att, B, d, 8, ss);
        }},
       {"argmax+embed", [=](hipStream_t ss) {
-         launch_dec_argmax(st, t, 0, logits, 0, Vp, V, B, ids, feed, nullptr, 151, logp, fin, 2, 0, W, W, x, d, ss);
+         launch_dec_argmax(sel(nullptr), 0, B, W, W, x, d, ss);
        }},
       {"logits + tile partials", [=](hipStream_t ss) {
          RowGemmParams p{};
@@ -106,12 +112,18 @@ int main(int argc, char** argv) {
          launch_rowgemm(p, ss);
        }},
       {"argmax (tile partials)+qkv", [=](hipStream_t ss) {
-         launch_dec_argmax(st, t, 0, logits, 0, Vp, V, B, ids, feed, nullptr, 151, logp, fin, 2, 0, W, W, x, d, ss,
-                           W, W, zb, part);
+         launch_dec_argmax(sel(part), 0, B, W, W, x, d, ss, W, W, zb);
        }},
       {"argmax+embed+qkv table", [=](hipStream_t ss) {
-         launch_dec_argmax(st, t, 0, logits, 0, Vp, V, B, ids, feed, nullptr, 151, logp, fin, 2, 0, W, W, x, d, ss,
-                           W, W, zb);
+         launch_dec_argmax(sel(nullptr), 0, B, W, W, x, d, ss, W, W, zb);
+       }},
+      {"fold self-attn t=100 + select of t-1 (tile partials)", [=](hipStream_t ss) {
+         FoldAttnParams a{};
+         a.t = t; a.B = B; a.out = att; a.z = zb; a.z_ld = 3 * d;
+         a.K = kc; a.V = vc; a.kcache = kc; a.vcache = vc; a.kv_b_stride = (size_t)P * d; a.kv_row_stride = d;
+         a.n = t + 1;
+         a.sel_on = 1; a.sel = sel(part); a.sel.t = t - 1; a.qtab = W; a.qpos = W; a.emb = W; a.pos = W; a.x = x;
+         launch_dec_foldattn(a, true, ss);
        }},
       {"fold self-attn t=100", [=](hipStream_t ss) {
          FoldAttnParams a{};
