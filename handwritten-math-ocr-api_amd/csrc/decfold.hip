@@ -92,7 +92,7 @@ __device__ __forceinline__ void fold_tile(const FoldGemmParams& p, int c0) {
   __shared__ float red[NW][16][17];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar branches on k ranges
   const int r0 = blockIdx.y * 16;
   const int ra = min(r0 + (lane & 15), p.B - 1);  // rows >= B compute discarded outputs
   const int cb = c0 + (lane & 15);
@@ -101,7 +101,25 @@ __device__ __forceinline__ void fold_tile(const FoldGemmParams& p, int c0) {
   const int K1 = p.K1;
   const float* wrow = YT ? p.Wy + (size_t)cb * K1 : p.Wz + (size_t)cb * (K1 + kD);
 
-  // every independent load first: A, W, the unfold / LayerNorm vectors, the residual
+  // The unfold / LayerNorm vectors depend on k only: the workgroup stages them in LDS
+  // (one float4 of each per thread, issued first) instead of every lane loading its own
+  // copies -- 16 lanes share each value, but a vector load returns 16 B per lane through
+  // the CU's load-data path either way, and these were half of the kernel's loads.
+  // (with S1; without it only the A2 quarter of a z tile needs LN vectors: per lane, below)
+  constexpr int KUV = NI * 16 * NW;  // this tile's K
+  constexpr bool UV = S1;
+  __shared__ floatx4 uv_s[2][UV ? KUV / 4 : 1];
+  floatx4 u4{}, v4{};
+  const int kk4 = min(tid * 4, KUV - 4);
+  if constexpr (UV) {
+    static_assert(KUV / 4 <= 64 * NW, "one float4 of u and of v per thread");
+    const bool in1 = kk4 < K1;
+    const float* us = in1 ? (S1 ? p.a1_s + kk4 : p.a2_g) : (S2 ? p.a2_g + (kk4 - K1) : p.a1_s);
+    const float* vs = in1 ? (S1 ? p.a1_c + kk4 : p.a2_b) : (S2 ? p.a2_b + (kk4 - K1) : p.a1_c);
+    u4 = *reinterpret_cast<const floatx4*>(us);
+    v4 = *reinterpret_cast<const floatx4*>(vs);
+  }
+  // every independent load first: A, W, the residual
   floatx4 a[NI], b[NI], u[NI], v[NI];
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
@@ -109,11 +127,24 @@ __device__ __forceinline__ void fold_tile(const FoldGemmParams& p, int c0) {
     const bool in1 = k < K1;
     b[i] = *reinterpret_cast<const floatx4*>(wrow + k);
     a[i] = *reinterpret_cast<const floatx4*>(in1 ? p.A1 + (size_t)ra * K1 + k : p.A2 + (size_t)ra * kD + (k - K1));
-    if constexpr (S1 || S2) {
-      const float* us = in1 ? (S1 ? p.a1_s + k : p.a2_g) : (S2 ? p.a2_g + (k - K1) : p.a1_s);
-      const float* vs = in1 ? (S1 ? p.a1_c + k : p.a2_b) : (S2 ? p.a2_b + (k - K1) : p.a1_c);
-      u[i] = *reinterpret_cast<const floatx4*>(us);
-      v[i] = *reinterpret_cast<const floatx4*>(vs);
+    if constexpr (S2 && !S1 && !YT) {
+      if (kbeg + i * 16 >= K1) {  // wave-uniform (K1 % 16 == 0): LN2 of the A2 columns
+        u[i] = *reinterpret_cast<const floatx4*>(p.a2_g + (k - K1));
+        v[i] = *reinterpret_cast<const floatx4*>(p.a2_b + (k - K1));
+      }
+    }
+  }
+  if constexpr (UV) {
+    if (tid * 4 < KUV) {
+      uv_s[0][kk4 / 4] = u4;
+      uv_s[1][kk4 / 4] = v4;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int k = kbeg + i * 16 + 4 * g;
+      u[i] = uv_s[0][k / 4];
+      v[i] = uv_s[1][k / 4];
     }
   }
   const int row = tid >> 4;

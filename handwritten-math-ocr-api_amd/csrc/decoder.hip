@@ -111,7 +111,15 @@ __global__ void __launch_bounds__(256) rowgemm_kernel(RowGemmParams p) {
   const bool row_ok = ra < p.B;
   const int rc = row_ok ? ra : p.B - 1;  // loads are never predicated (see dec_argmax_kernel)
 
-  // issue every independent load first: A, W, LayerNorm affine, residual
+  // issue every independent load first: the LayerNorm affine (one float4 of each per
+  // thread, staged in LDS: 16 lanes share every value), A, W, residual
+  __shared__ floatx4 gb_s[2][ALN ? kD / 4 : 1];
+  floatx4 g4{}, b4{};
+  if constexpr (ALN) {  // K == d == 256: 64 float4 of each
+    const int k4 = (tid & 63) * 4;
+    g4 = *reinterpret_cast<const floatx4*>(p.a_ln_g + k4);
+    b4 = *reinterpret_cast<const floatx4*>(p.a_ln_b + k4);
+  }
   floatx4 a[NI], b[NI];
   floatx4 gg[ALN ? NI : 1], bb[ALN ? NI : 1];
 #pragma unroll
@@ -120,9 +128,18 @@ __global__ void __launch_bounds__(256) rowgemm_kernel(RowGemmParams p) {
     a[i] = *reinterpret_cast<const floatx4*>(p.A + (size_t)rc * p.K + k);
     if (!row_ok) a[i] = floatx4{0.f, 0.f, 0.f, 0.f};
     b[i] = *reinterpret_cast<const floatx4*>(p.W + (size_t)cb * p.K + k);
-    if constexpr (ALN) {
-      gg[i] = *reinterpret_cast<const floatx4*>(p.a_ln_g + k);
-      bb[i] = *reinterpret_cast<const floatx4*>(p.a_ln_b + k);
+  }
+  if constexpr (ALN) {
+    if (tid < 64) {
+      gb_s[0][tid] = g4;
+      gb_s[1][tid] = b4;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int k = kbeg + i * 16 + 4 * g;
+      gg[i] = gb_s[0][k / 4];
+      bb[i] = gb_s[1][k / 4];
     }
   }
   const int row = tid >> 4;
