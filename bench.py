@@ -143,7 +143,7 @@ def roofline(stats, dtype, precision):
 
 
 def roofline_decode(stats, precision):
-    """The greedy decode step (42 graph-captured dependent kernels) against HBM: the
+    """The greedy decode step (41 graph-captured dependent kernels) against HBM: the
     algorithmic bytes of a step (engine.hip decode_step_bytes: weights, cross-attention
     K/V, self-attention K/V, logits; fp32 as built) / the HIP-event step time."""
     d = stats.get("decode.greedy")
@@ -152,7 +152,7 @@ def roofline_decode(stats, precision):
     step_ms = d["total_ms"] / d["launches"]
     byts = d["bytes"] / d["launches"]
     achieved = byts / (step_ms * 1e-3) / 1e9
-    return {"kernel": "greedy decode step (8 layers x 5 folded kernels + logits + argmax)", "bound": "hbm",
+    return {"kernel": "greedy decode step (8 layers x 5 folded kernels + logits; the selection runs in the next step's first kernel)", "bound": "hbm",
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
             "traffic": pmc_traffic(precision, "decode.step"), "avg_step_ms": step_ms,
             "algorithmic_bytes_per_step": byts, "tflops": d["flops"] / d["launches"] / (step_ms * 1e-3) / 1e12}

@@ -424,6 +424,7 @@ struct mocr_engine {
     }
     rzero = dalloc<char>(256);
     MOCR_HIP_CHECK(hipMemset(rzero, 0, 256));
+    MOCR_HIP_CHECK(hipDeviceSynchronize());  // null-stream memset vs the engine's non-blocking stream
     RP = dalloc<float>(rows * 512);
     RPOS = dalloc<float>((size_t)M * d);
     RPOSB = dalloc<float>(rows * d);
@@ -496,6 +497,7 @@ struct mocr_engine {
       auto up = [&](const ConvW& c, DevConv& dc) {
         fold_bn(blob, c, w, bias);
         MOCR_HIP_CHECK(hipMemcpy(tmp, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+        MOCR_HIP_CHECK(hipDeviceSynchronize());  // before the non-blocking stream reads tmp
         launch_split_bf16(tmp, dc.wh, dc.wl, w.size(), stream);
         MOCR_HIP_CHECK(hipStreamSynchronize(stream));
         MOCR_HIP_CHECK(hipMemcpy(dc.bias, bias.data(), bias.size() * 4, hipMemcpyHostToDevice));
@@ -513,6 +515,7 @@ struct mocr_engine {
                                               "makes " + std::to_string(M) + " tokens");
     MOCR_HIP_CHECK(hipSetDevice(device));
     MOCR_HIP_CHECK(hipMemcpy(RPOS, table, (size_t)M * cfg.d_model * 4, hipMemcpyHostToDevice));
+    MOCR_HIP_CHECK(hipDeviceSynchronize());  // visible to the engine's non-blocking stream
     pos_set = true;
     encoded = false;
   }
@@ -835,17 +838,21 @@ struct mocr_engine {
         if (relmask[bi]) build_relmask(rb, h, stage[s].win[j & 1], relmask[bi]);
       }
     }
+    // Everything below runs on the engine's stream, ordered behind the uploads above: the
+    // stream is non-blocking, so null-stream memsets / device-to-device copies (which may
+    // return before they complete) would race the split kernels that read them.
+    MOCR_HIP_CHECK(hipDeviceSynchronize());
     const size_t d = cfg.d_model, V = cfg.vocab;
-    MOCR_HIP_CHECK(hipMemset(fcw_pad, 0, (size_t)Vpad * d * sizeof(float)));
-    MOCR_HIP_CHECK(hipMemset(fcb_pad, 0, (size_t)Vpad * sizeof(float)));
-    MOCR_HIP_CHECK(hipMemcpy(fcw_pad, dw + lay->fcw, V * d * sizeof(float), hipMemcpyDeviceToDevice));
-    MOCR_HIP_CHECK(hipMemcpy(fcb_pad, dw + lay->fcb, V * sizeof(float), hipMemcpyDeviceToDevice));
+    MOCR_HIP_CHECK(hipMemsetAsync(fcw_pad, 0, (size_t)Vpad * d * sizeof(float), stream));
+    MOCR_HIP_CHECK(hipMemsetAsync(fcb_pad, 0, (size_t)Vpad * sizeof(float), stream));
+    MOCR_HIP_CHECK(hipMemcpyAsync(fcw_pad, dw + lay->fcw, V * d * sizeof(float), hipMemcpyDeviceToDevice, stream));
+    MOCR_HIP_CHECK(hipMemcpyAsync(fcb_pad, dw + lay->fcb, V * sizeof(float), hipMemcpyDeviceToDevice, stream));
     for (int l = 0; l < cfg.n_layers; ++l) {
       const DecLayerW& w = lay->layers[l];
-      MOCR_HIP_CHECK(hipMemcpy(kvw_all + (size_t)l * 2 * d * d, dw + w.ca_inw + d * d, 2 * d * d * sizeof(float),
-                               hipMemcpyDeviceToDevice));
-      MOCR_HIP_CHECK(hipMemcpy(kvb_all + (size_t)l * 2 * d, dw + w.ca_inb + d, 2 * d * sizeof(float),
-                               hipMemcpyDeviceToDevice));
+      MOCR_HIP_CHECK(hipMemcpyAsync(kvw_all + (size_t)l * 2 * d * d, dw + w.ca_inw + d * d, 2 * d * d * sizeof(float),
+                                    hipMemcpyDeviceToDevice, stream));
+      MOCR_HIP_CHECK(hipMemcpyAsync(kvb_all + (size_t)l * 2 * d, dw + w.ca_inb + d, 2 * d * sizeof(float),
+                                    hipMemcpyDeviceToDevice, stream));
     }
     if (dwh) {
       launch_split_bf16(dw, dwh, dwl, lay->total, stream);
@@ -1093,13 +1100,14 @@ struct mocr_engine {
           ap.table = relmask[bi];
           ap.att_hi = ATTh;
           ap.att_lo = dwl ? ATTl : nullptr;
+          ap.att_pixel_rows = 1;  // O in X's row order: proj over the image's tokens only
           ap.B = B;
           ap.C = C;
           ap.heads = g.heads;
           ap.wg = wg;
           timed(attn_n[s], 6.0 * rows * C * C + 4.0 * rows * kWinTok * C, 4.0 * rows * C + (dwl ? 4.0 : 2.0) * 3.0 * C * C +
                 (dwl ? 4.0 : 2.0) * rows * C, [&] { launch_swin_attn_noproj(ap, stream); });
-          gemm(proj_n[s], opATT, wop(w.projw), W(w.projb), X, nullptr, nullptr, (int)wrows, C, C, EPI_WINRES, &wg,
+          gemm(proj_n[s], opATT, wop(w.projw), W(w.projb), X, nullptr, nullptr, (int)rows, C, C, EPI_RESADD, nullptr,
                rows);
         } else {
           timed(ln1_n[s], 0, 8.0 * wrows * C,
@@ -1564,8 +1572,9 @@ struct mocr_engine {
     const int B = cur_batch, ld = ld_ids, Wd = max_steps + 1;
     std::vector<int32_t> seq((size_t)B * K * ld);
     std::vector<float> sc((size_t)B * K);
-    MOCR_HIP_CHECK(hipMemcpy(seq.data(), bseq[n & 1], seq.size() * 4, hipMemcpyDeviceToHost));
-    MOCR_HIP_CHECK(hipMemcpy(sc.data(), bscore, sc.size() * 4, hipMemcpyDeviceToHost));
+    MOCR_HIP_CHECK(hipMemcpyAsync(seq.data(), bseq[n & 1], seq.size() * 4, hipMemcpyDeviceToHost, stream));
+    MOCR_HIP_CHECK(hipMemcpyAsync(sc.data(), bscore, sc.size() * 4, hipMemcpyDeviceToHost, stream));
+    MOCR_HIP_CHECK(hipStreamSynchronize(stream));
     for (int r = 0; r < B * K; ++r)
       for (int j = 0; j < Wd; ++j) {
         const int32_t v = j <= n ? seq[(size_t)r * ld + j] : cfg.pad_id;
@@ -1701,8 +1710,10 @@ int mocr_get_memory(mocr_engine* eng, float* host_out) {
   MOCR_API_BODY(eng, {
     if (!eng->encoded) throw std::runtime_error("not encoded");
     MOCR_HIP_CHECK(hipSetDevice(eng->device));
-    MOCR_HIP_CHECK(hipMemcpy(host_out, eng->MEM, (size_t)eng->cur_batch * eng->M * eng->cfg.d_model * sizeof(float),
-                             hipMemcpyDeviceToHost));
+    MOCR_HIP_CHECK(hipMemcpyAsync(host_out, eng->MEM,
+                                  (size_t)eng->cur_batch * eng->M * eng->cfg.d_model * sizeof(float),
+                                  hipMemcpyDeviceToHost, eng->stream));
+    MOCR_HIP_CHECK(hipStreamSynchronize(eng->stream));
   })
 }
 
@@ -1751,7 +1762,8 @@ int mocr_debug_encode_until(mocr_engine* eng, int batch, int k, float* host_out,
     if (k < 0 || k > 7) throw std::runtime_error("k must be in [0, 7]");
     eng->encode(batch, k);
     if (n != eng->stage_elems(k)) throw std::runtime_error("wrong output size for stage " + std::to_string(k));
-    MOCR_HIP_CHECK(hipMemcpy(host_out, eng->X, n * sizeof(float), hipMemcpyDeviceToHost));
+    MOCR_HIP_CHECK(hipMemcpyAsync(host_out, eng->X, n * sizeof(float), hipMemcpyDeviceToHost, eng->stream));
+    MOCR_HIP_CHECK(hipStreamSynchronize(eng->stream));
   })
 }
 

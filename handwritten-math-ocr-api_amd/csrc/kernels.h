@@ -121,7 +121,9 @@ struct SwinAttnParams {
   const void *wproj, *wproj_lo;  // [C, C]
   const float* bproj;         // [C]
   const float* table;         // [4 window types][heads][64 q][64 key] bias + mask (build_relmask)
-  uint16_t *att_hi, *att_lo;  // noproj: O planes [B * nWin * 49, C] (window-token rows)
+  uint16_t *att_hi, *att_lo;  // noproj: O planes [B * nWin * 49, C] (window-token rows), or
+                              // att_pixel_rows: [B * H * W, C] in X's row order, padding dropped
+  int att_pixel_rows;
   int B, C, heads;
   WinGeom wg;
 };

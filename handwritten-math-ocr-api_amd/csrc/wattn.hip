@@ -457,7 +457,8 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
 template <bool X3, int C>
 __device__ __forceinline__ void attend_to_planes(const bf16x8 (&kf)[4][2], const bf16x8 (&vf)[2][2][2],
                                                  const bf16x8 (&qf4)[4][2], const float* tb, int j16, int g,
-                                                 size_t tok0, int ch0, uint16_t* att_hi, uint16_t* att_lo) {
+                                                 const long (&orow)[4], int ch0, uint16_t* att_hi,
+                                                 uint16_t* att_lo) {
   floatx4 bm[4];  // bias + mask of the current query tile
 #pragma unroll
   for (int kt = 0; kt < 4; ++kt) bm[kt] = *reinterpret_cast<const floatx4*>(tb + j16 * 64 + 16 * kt + 4 * g);
@@ -513,12 +514,12 @@ __device__ __forceinline__ void attend_to_planes(const bf16x8 (&kf)[4][2], const
       x[r] = o[0][r] * inv;
       x[4 + r] = o[1][r] * inv;
     }
-    // ATT planes [window token row, C]: token 16qt + j16, channels 32h + {4g.., 16+4g..}
-    const int q = 16 * qt + j16;
-    if (q < kWinTok) {
+    // ATT planes [row, C]: query token 16qt + j16 -> row orow[qt] (-1: not written),
+    // channels 32h + {4g.., 16+4g..}
+    if (orow[qt] >= 0) {
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
-        const size_t off = (tok0 + q) * C + ch0 + 16 * dt + 4 * g;
+        const size_t off = (size_t)orow[qt] * C + ch0 + 16 * dt + 4 * g;
         uint32_t h0, l0, h1, l1;
         split2_bf16(x[4 * dt], x[4 * dt + 1], h0, l0);
         split2_bf16(x[4 * dt + 2], x[4 * dt + 3], h1, l1);
@@ -661,6 +662,15 @@ swin_attn_noproj_kernel(SwinAttnParams p) {
     }
   };
 
+  // destination row of each of this lane's 4 query tokens: the pixel row (window reverse,
+  // un-roll and crop, padded tokens dropped: proj is then a plain residual-add GEMM over
+  // the image's tokens), or the window-token row (the EPI_WINRES proj)
+  long orow[4];
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {
+    const int q = 16 * qt + j16;
+    orow[qt] = p.att_pixel_rows ? pixel(q) : (q < kWinTok ? ((long)b * wg.nWin + win) * kWinTok + q : -1L);
+  }
 #pragma unroll 1
   for (int h = wave; h < HEADS; h += WAVES) {
     bf16x8 kf[4][2], vf[2][2][2], qf4[4][2];
@@ -732,8 +742,8 @@ swin_attn_noproj_kernel(SwinAttnParams p) {
     // ---- C: attention per 16-query tile
     int type = 0;
     if (wg.sh + wg.sw > 0) type = 2 * (wy == wg.nWin / wg.nWx - 1) + (wx == wg.nWx - 1);
-    attend_to_planes<X3, C>(kf, vf, qf4, p.table + ((size_t)type * HEADS + h) * 64 * 64, j16, g,
-                            (size_t)((long)b * wg.nWin + win) * kWinTok, 32 * h, p.att_hi, p.att_lo);
+    attend_to_planes<X3, C>(kf, vf, qf4, p.table + ((size_t)type * HEADS + h) * 64 * 64, j16, g, orow, 32 * h,
+                            p.att_hi, p.att_lo);
   }
 }
 
@@ -940,8 +950,17 @@ swin_attn_noproj_ks_kernel(SwinAttnParams p) {
   // ---- C
   int type = 0;
   if (wg.sh + wg.sw > 0) type = 2 * (wy == wg.nWin / wg.nWx - 1) + (wx == wg.nWx - 1);
-  attend_to_planes<X3, C>(kf, vf, qf4, p.table + ((size_t)type * HEADS + h) * 64 * 64, j16, g,
-                          (size_t)((long)b * wg.nWin + win) * kWinTok, 32 * h, p.att_hi, p.att_lo);
+  // destination row of each of this lane's 4 query tokens: the pixel row (window reverse,
+  // un-roll and crop, padded tokens dropped: proj is then a plain residual-add GEMM over
+  // the image's tokens), or the window-token row (the EPI_WINRES proj)
+  long orow[4];
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {
+    const int q = 16 * qt + j16;
+    orow[qt] = p.att_pixel_rows ? pixel(q) : (q < kWinTok ? ((long)b * wg.nWin + win) * kWinTok + q : -1L);
+  }
+  attend_to_planes<X3, C>(kf, vf, qf4, p.table + ((size_t)type * HEADS + h) * 64 * 64, j16, g, orow, 32 * h,
+                          p.att_hi, p.att_lo);
 }
 
 template <int C, int OCC>
