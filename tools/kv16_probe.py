@@ -1,0 +1,58 @@
+"""CPU precision probe (test infrastructure, imports the oracle): teacher-forced logits of
+the fixture batches with the decoder's K/V (self and cross attention) rounded to fp16 or
+bf16, against fp32.  Reports max |d logits| and the argmax flips against the fixture
+margins.   python tools/kv16_probe.py [fixture ...]
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import importlib  # noqa: E402
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from oracle import model_ref  # noqa: E402
+from oracle.gen_golden import apply_eos_boost  # noqa: E402
+from tests.conftest import load_golden  # noqa: E402
+
+pkg = importlib.import_module("handwritten-math-ocr-api_amd")
+_orig = F._in_projection_packed
+MODE = {"dt": None}
+
+
+def patched(q, k, v, w, b=None):
+    qq, kk, vv = _orig(q, k, v, w, b)
+    if MODE["dt"] is not None:
+        kk = kk.to(MODE["dt"]).float()
+        vv = vv.to(MODE["dt"]).float()
+    return qq, kk, vv
+
+
+F._in_projection_packed = patched
+names = sys.argv[1:] or ["g384_b2_pert", "g384_b1_init", "g96x320_b4_eos"]
+for name in names:
+    g = load_golden(name)
+    m = g["meta"]
+    w = pkg.synth.make_weights(m["seed"], m["variant"])
+    if m.get("eos_boost"):
+        w = apply_eos_boost(w, m["eos_boost"])
+    model = model_ref.build_model(w)
+    mem = torch.from_numpy(g["memory"]) if "memory" in g and g["memory"].ndim == 3 else None
+    if mem is None or mem.shape[0] != g["ids"].shape[0]:
+        imgs = pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m.get("img_kind", "uniform"))
+        mem = model_ref.encode(model, torch.from_numpy(imgs))
+    ys = torch.from_numpy(g["ids"]).long()
+    MODE["dt"] = None
+    ref = model_ref.teacher_forced_logits(model, mem, ys)
+    marg = model_ref.top2_margins(ref)
+    for dt in (torch.float16, torch.bfloat16):
+        MODE["dt"] = dt
+        out = model_ref.teacher_forced_logits(model, mem, ys)
+        d = (out - ref).abs().max().item()
+        flips = (out.argmax(-1) != ref.argmax(-1)).numpy()
+        fm = marg[flips] if flips.any() else np.array([])
+        print(f"{name}: K/V {str(dt)[6:]}: max|d logits| {d:.2e}, argmax flips {int(flips.sum())} of {flips.size} "
+              f"(their fp32 top-2 margins: {np.round(fm, 6).tolist()[:6]}), "
+              f"steps with margin < 1e-4: {int((marg < 1e-4).sum())}", flush=True)
