@@ -1,12 +1,12 @@
 """CPU precision probe (test infrastructure, imports the oracle): teacher-forced logits of
 the fixture batches with the decoder's K/V (self and cross attention) rounded to fp16 or
 bf16, against fp32.  Reports max |d logits| and the argmax flips against the fixture
-margins.   python tools/kv16_probe.py [fixture ...]
+margins.   python tests/probes/kv16_probe.py [fixture ...]
 """
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import importlib  # noqa: E402
 
 import numpy as np  # noqa: E402

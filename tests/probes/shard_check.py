@@ -1,13 +1,13 @@
 """Debug aid: the sharded-test fixture (g96x320_b4_eos) decoded at B=4 and as two B=2
 shards in one process, compared with the fixture ids; prints the first mismatch per row.
-    python tools/shard_check.py [--lib path/libmathocr.so]
+    python tests/probes/shard_check.py [--lib path/libmathocr.so]
 """
 import argparse
 import importlib
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402,F401
 
