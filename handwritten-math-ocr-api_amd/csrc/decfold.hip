@@ -26,6 +26,18 @@ namespace {
 constexpr int kD = 256;
 constexpr int kSlices = kD / 16;
 constexpr float kAttnScale = 0.17677669529663687f;  // 1/sqrt(32)
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// 8 floats -> bf16 hi / lo planes (split2_bf16 per pair): the A fragment of a bf16x3 MFMA
+__device__ __forceinline__ void split8(const floatx4& x0, const floatx4& x1, bf16x8& hi, bf16x8& lo) {
+  uint32_t h[4], l[4];
+  split2_bf16(x0[0], x0[1], h[0], l[0]);
+  split2_bf16(x0[2], x0[3], h[1], l[1]);
+  split2_bf16(x1[0], x1[1], h[2], l[2]);
+  split2_bf16(x1[2], x1[3], h[3], l[3]);
+  hi = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
+  lo = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
+}
 
 __device__ __forceinline__ float ln_apply(float v, float mean, float rstd, float g, float b) {
   return fmaf((v - mean) * rstd, g, b);
@@ -87,7 +99,11 @@ __device__ __forceinline__ void row_stats_16lanes(const float* __restrict__ part
 // DEC_RESADD (y = A2' + (acc + by), then the (mean, M2) of the tile's 16 columns).  The
 // 16-wide k chunks never straddle A1 / A2 (K1 % 16 == 0), so a chunk's source is
 // wave-uniform.  S1 / S2: A1 / A2 carry statistics (unfold / LayerNorm on load).
-template <int NI, bool YT, bool S1, bool S2, int NW>
+// X3: bf16x3 on v_mfma_f32_16x16x32_bf16 (Wy / Wz as bf16 hi / lo planes, A split on
+// load): a lane takes k = 32 s + 8 g .. +7 of its row / column per 32-deep step instead
+// of k = 16 i + 4 g .. +3 per 16-deep chunk; the transforms, reductions and epilogue are
+// the fp32 path's.
+template <int NI, bool YT, bool S1, bool S2, int NW, bool X3>
 __device__ __forceinline__ void fold_tile(const FoldGemmParams& p, int c0) {
   __shared__ float red[NW][16][17];
   const int tid = threadIdx.x;
@@ -119,16 +135,32 @@ __device__ __forceinline__ void fold_tile(const FoldGemmParams& p, int c0) {
     u4 = *reinterpret_cast<const floatx4*>(us);
     v4 = *reinterpret_cast<const floatx4*>(vs);
   }
-  // every independent load first: A, W, the residual
-  floatx4 a[NI], b[NI], u[NI], v[NI];
+  // every independent load first: A, W, the residual.  Slot i holds 4 consecutive k:
+  // fp32, k = 16 i + 4 g (one 16x16x4 chunk); bf16x3, k = 32 (i / 2) + 8 g + 4 (i % 2)
+  // (the two halves of a 32-deep step's 8 k)
+  auto kof = [&](int i) { return X3 ? kbeg + 32 * (i >> 1) + 8 * g + 4 * (i & 1) : kbeg + i * 16 + 4 * g; };
+  floatx4 a[NI], b[X3 ? 1 : NI], u[NI], v[NI];
+  bf16x8 bh[X3 ? NI / 2 : 1], bl[X3 ? NI / 2 : 1];
+  if constexpr (X3) {
+    static_assert(NI % 2 == 0, "32-deep steps");
+    const size_t wo = (size_t)cb * (YT ? K1 : K1 + kD);
+    const uint16_t* whr = (YT ? p.Wy_hi : p.Wz_hi) + wo;
+    const uint16_t* wlr = (YT ? p.Wy_lo : p.Wz_lo) + wo;
+#pragma unroll
+    for (int s2 = 0; s2 < NI / 2; ++s2) {
+      const int k = kbeg + 32 * s2 + 8 * g;
+      bh[s2] = *reinterpret_cast<const bf16x8*>(whr + k);
+      bl[s2] = *reinterpret_cast<const bf16x8*>(wlr + k);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
-    const int k = kbeg + i * 16 + 4 * g;
-    const bool in1 = k < K1;
-    b[i] = *reinterpret_cast<const floatx4*>(wrow + k);
+    const int k = kof(i);
+    const bool in1 = k < K1;  // uniform per slot: K1 % 32 == 0
+    if constexpr (!X3) b[i] = *reinterpret_cast<const floatx4*>(wrow + k);
     a[i] = *reinterpret_cast<const floatx4*>(in1 ? p.A1 + (size_t)ra * K1 + k : p.A2 + (size_t)ra * kD + (k - K1));
     if constexpr (S2 && !S1 && !YT) {
-      if (kbeg + i * 16 >= K1) {  // wave-uniform (K1 % 16 == 0): LN2 of the A2 columns
+      if ((X3 ? kbeg + 32 * (i >> 1) : kbeg + 16 * i) >= K1) {  // wave-uniform: LN2 of the A2 columns
         u[i] = *reinterpret_cast<const floatx4*>(p.a2_g + (k - K1));
         v[i] = *reinterpret_cast<const floatx4*>(p.a2_b + (k - K1));
       }
@@ -142,7 +174,7 @@ __device__ __forceinline__ void fold_tile(const FoldGemmParams& p, int c0) {
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int k = kbeg + i * 16 + 4 * g;
+      const int k = kof(i);
       u[i] = uv_s[0][k / 4];
       v[i] = uv_s[1][k / 4];
     }
@@ -170,7 +202,7 @@ __device__ __forceinline__ void fold_tile(const FoldGemmParams& p, int c0) {
   if constexpr (S1 || S2) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int k = kbeg + i * 16 + 4 * g;
+      const int k = kof(i);
       if (k < K1) {
         if constexpr (S1)
 #pragma unroll
@@ -184,10 +216,21 @@ __device__ __forceinline__ void fold_tile(const FoldGemmParams& p, int c0) {
   }
 
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (X3) {
 #pragma unroll
-  for (int i = 0; i < NI; ++i)
+    for (int s2 = 0; s2 < NI / 2; ++s2) {
+      bf16x8 ah, al;
+      split8(a[2 * s2], a[2 * s2 + 1], ah, al);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[s2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[s2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[s2], acc, 0, 0, 0);
+    }
+  } else {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[i][s], acc, 0, 0, 0);
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[i][s], acc, 0, 0, 0);
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) red[wave][g * 4 + r][lane & 15] = acc[r];
   __syncthreads();
@@ -226,12 +269,12 @@ __device__ __forceinline__ void fold_tile(const FoldGemmParams& p, int c0) {
 }
 
 // NW waves split K (4 or 8: 512-thread workgroups halve each wave's load chain).
-template <int K1, bool S1, bool S2, int NW>
+template <int K1, bool S1, bool S2, int NW, bool X3>
 __global__ void __launch_bounds__(64 * NW) foldgemm_kernel(FoldGemmParams p) {
   if (blockIdx.x < kD / 16)
-    fold_tile<K1 / (16 * NW), true, S1, S2, NW>(p, blockIdx.x * 16);
+    fold_tile<K1 / (16 * NW), true, S1, S2, NW, X3>(p, blockIdx.x * 16);
   else
-    fold_tile<(K1 + kD) / (16 * NW), false, S1, S2, NW>(p, (blockIdx.x - kD / 16) * 16);
+    fold_tile<(K1 + kD) / (16 * NW), false, S1, S2, NW, X3>(p, (blockIdx.x - kD / 16) * 16);
 }
 
 // ------------------------------------------------------------------ fold attention
@@ -430,7 +473,14 @@ void launch_foldgemm(const FoldGemmParams& p, hipStream_t s) {
   if (p.B <= 0) return;
   const dim3 grid(kD / 16 + p.NZ / 16, (p.B + 15) / 16);
   // 4 waves split K (8-wave workgroups measured no faster)
-#define MOCR_FG(K1, S1, S2) foldgemm_kernel<K1, S1, S2, 4><<<grid, 256, 0, s>>>(p);
+  const bool x3 = p.Wy_hi != nullptr;
+  if (x3 && (!p.Wy_lo || (p.NZ && (!p.Wz_hi || !p.Wz_lo))))
+    throw std::runtime_error("foldgemm: bf16x3 needs hi and lo planes of Wy and Wz");
+#define MOCR_FG(K1, S1, S2)                                      \
+  if (x3)                                                        \
+    foldgemm_kernel<K1, S1, S2, 4, true><<<grid, 256, 0, s>>>(p); \
+  else                                                           \
+    foldgemm_kernel<K1, S1, S2, 4, false><<<grid, 256, 0, s>>>(p);
   if (p.K1 == 256 && !s1 && !s2) {
     MOCR_FG(256, false, false)
   } else if (p.K1 == 256 && !s1 && s2) {

@@ -334,6 +334,8 @@ struct mocr_engine {
   };
   std::vector<FoldW> foldw;
   float* fold_buf = nullptr;
+  size_t fold_floats = 0;
+  uint16_t *fold_h = nullptr, *fold_l = nullptr;  // bf16x3: hi / lo planes of fold_buf
   float *qtab = nullptr, *qpos = nullptr, *dzqkv = nullptr;
   float* dpart = nullptr;  // greedy: logits tile partials [rows][Vpad/16] float4 for the argmax
 
@@ -748,6 +750,11 @@ struct mocr_engine {
       const size_t ff = cfg.d_ff;
       const size_t per = 2 * d * d + 3 * d + ff * 2 * d + 3 * ff + 3 * d * (ff + d) + 9 * d;
       fold_buf = dalloc<float>(per * L);
+      fold_floats = per * L;
+      if (cfg.precision == MOCR_PRECISION_BF16X3 && dwl) {  // the Swin engine's blob planes exist
+        fold_h = dalloc<uint16_t>(per * L);
+        fold_l = dalloc<uint16_t>(per * L);
+      }
       foldw.resize(L);
       float* f = fold_buf;
       auto take = [&](size_t n) {
@@ -903,6 +910,7 @@ struct mocr_engine {
     launch_fold_mm(W(lay->emb), d, nullptr, W(l0.sa_inw), 1, d, d, nullptr, W(l0.sa_inb), qtab, 3 * d, cfg.vocab,
                    3 * d, s);
     launch_fold_mm(W(lay->pos), d, nullptr, W(l0.sa_inw), 1, d, d, nullptr, nullptr, qpos, 3 * d, cfg.max_pos, 3 * d, s);
+    if (fold_h) launch_split_bf16(fold_buf, fold_h, fold_l, fold_floats, s);
     MOCR_HIP_CHECK(hipStreamSynchronize(s));
   }
 
@@ -1286,6 +1294,19 @@ struct mocr_engine {
     }
   }
 
+  // bf16x3 engines run the fold GEMMs on bf16x3 MFMA: Wy's planes are the blob's (dwh /
+  // dwl at the blob offset), Wz's the split of the folded weights
+  void fold_planes(FoldGemmParams& g, size_t wy_off) const {
+    if (!fold_h) return;
+    g.Wy_hi = dwh + wy_off;
+    g.Wy_lo = dwl + wy_off;
+    if (g.NZ) {
+      const size_t zo = (size_t)(g.Wz - fold_buf);
+      g.Wz_hi = fold_h + zo;
+      g.Wz_lo = fold_l + zo;
+    }
+  }
+
   // The folded greedy step (kernels.h FoldGemmParams): per layer 5 dependent kernels --
   // self-attention (q|k|v unfolded from dzqkv: layer 0's from the embedding tables, later
   // layers' from the previous FFN kernel), out_proj + z_q, cross-attention (q unfolded),
@@ -1318,6 +1339,7 @@ struct mocr_engine {
       if (l) { g.a2_stats = ds_ff; g.a2_g = W(prev->n3w); g.a2_b = W(prev->n3b); }
       g.Wy = W(w.sa_ow); g.by = W(w.sa_ob); g.y = dy_sa; g.y_stats = ds_sa;
       g.Wz = f.wzq; g.bz = f.bzq; g.z = dq; g.NZ = d;
+      fold_planes(g, w.sa_ow);
       launch_foldgemm(g, s);
       // y_ca = LN1(y_sa) + CA(LN1(y_sa), mem): attention, then out_proj + z_h = W_1' y_ca
       const float* memk = MEMKV + l * kv_layer;
@@ -1330,6 +1352,7 @@ struct mocr_engine {
       g.A1 = datt; g.K1 = d; g.A2 = dy_sa; g.a2_stats = ds_sa; g.a2_g = W(w.n1w); g.a2_b = W(w.n1b);
       g.Wy = W(w.ca_ow); g.by = W(w.ca_ob); g.y = dy_ca; g.y_stats = ds_ca;
       g.Wz = f.wzh; g.bz = f.bzh; g.z = dh; g.NZ = cfg.d_ff;
+      fold_planes(g, w.ca_ow);
       launch_foldgemm(g, s);
       // y_ff = LN2(y_ca) + W_2 relu(unfold(z_h)) + b_2, and the next layer's z_qkv
       g = FoldGemmParams{};
@@ -1338,6 +1361,7 @@ struct mocr_engine {
       g.A2 = dy_ca; g.a2_stats = ds_ca; g.a2_g = W(w.n2w); g.a2_b = W(w.n2b);
       g.Wy = W(w.l2w); g.by = W(w.l2b); g.y = dy_ff; g.y_stats = ds_ff;
       if (l + 1 < L) { g.Wz = f.wzqkv; g.bz = f.bzqkv; g.z = dzqkv; g.NZ = 3 * d; }
+      fold_planes(g, w.l2w);
       launch_foldgemm(g, s);
     }
   }

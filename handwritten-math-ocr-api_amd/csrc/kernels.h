@@ -197,6 +197,9 @@ struct FoldGemmParams {
   int NZ;
   int B, t;
   const DecodeState* st;
+  // bf16x3 (optional): bf16 hi / lo planes of Wy and Wz; A is split on load and each
+  // product is hi·hi + hi·lo + lo·hi on v_mfma_f32_16x16x32_bf16 (fp32 MFMA otherwise)
+  const uint16_t *Wy_hi, *Wy_lo, *Wz_hi, *Wz_lo;
 };
 void launch_foldgemm(const FoldGemmParams& p, hipStream_t s);
 

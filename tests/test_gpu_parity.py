@@ -97,6 +97,26 @@ def test_teacher_forced_logits_384(pkg, g384):
     np.testing.assert_array_equal(res.ids[:, 1:], g["ids"][:, 1:])
 
 
+@pytest.mark.parametrize("name", ["g384_b2_pert", "g96x320_b4_eos"])
+def test_teacher_forced_logits_bf16x3(pkg, golden, name):
+    """The bench precision (bf16x3 encoder GEMMs, attention and fold GEMMs of the decode
+    step): teacher-forced logits within the north star's 1e-3, ids token-exact."""
+    g = golden(name)
+    m = g["meta"]
+    eng, _ = make_engine(pkg, m, precision="bf16x3")
+    eng.encode(pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m["img_kind"]))
+    S = g["ids"].shape[1] - 1
+    res = eng.decode(max_steps=S, stop="none", forced=g["ids"], want_logits=True)
+    eng.close()
+    n = g["logits"].shape[1]
+    err = float(np.abs(res.logits[:, :n] - g["logits"]).max())
+    print(f"{name} bf16x3 teacher-forced logits max|d| = {err:.2e}")
+    assert err < LOGIT_TOL, err
+    margins = g["margins"]
+    ok = margins >= 1e-4  # near-ties a different fp32 summation order may flip (DESIGN §4)
+    assert np.array_equal(res.ids[:, 1:][ok], g["ids"][:, 1:][ok])
+
+
 def test_unfolded_decode_variant_matches_golden(pkg, golden):
     """MOCR_VARIANT_DEC_UNFOLDED: the 8-kernel greedy step (LayerNorms applied by their
     consumers) gives the fixture's ids and teacher-forced logits, as the folded step does."""

@@ -72,9 +72,11 @@ int main(int argc, char** argv) {
   float* zb = alloc<float>(B * 768);
   float* part = alloc<float>(B * Vp / 4);
   float* wz = alloc<float>((size_t)768 * 768);
-  auto fg = [&](int K1, int NZ, bool s1) {
+  uint16_t* w16 = alloc<uint16_t>((size_t)768 * 768);
+  auto fg = [&](int K1, int NZ, bool s1, bool x3 = false) {
     return [=](hipStream_t ss) {
       FoldGemmParams p{};
+      if (x3) { p.Wy_hi = w16; p.Wy_lo = w16; p.Wz_hi = w16; p.Wz_lo = w16; }
       p.B = B; p.t = t; p.A1 = x; p.K1 = K1; p.A2 = q; p.a2_stats = stats; p.a2_g = g; p.a2_b = g;
       if (s1) { p.a1_stats = stats; p.a1_s = g; p.a1_c = g; }
       p.Wy = W; p.by = bias; p.y = y; p.y_stats = stats2; p.Wz = wz; p.bz = bias; p.z = zb; p.NZ = NZ;
@@ -148,6 +150,9 @@ int main(int argc, char** argv) {
       {"foldgemm y256+z256 K1=256 +LN", fg(256, 256, false)},
       {"foldgemm y256+z512 K1=256 +LN", fg(256, 512, false)},
       {"foldgemm y256+z768 K1=512 +unf", fg(512, 768, true)},
+      {"foldgemm y256+z256 K1=256 +LN bf16x3", fg(256, 256, false, true)},
+      {"foldgemm y256+z512 K1=256 +LN bf16x3", fg(256, 512, false, true)},
+      {"foldgemm y256+z768 K1=512 +unf bf16x3", fg(512, 768, true, true)},
   };
   const int chain = 200;
   for (auto& c : cases) {
