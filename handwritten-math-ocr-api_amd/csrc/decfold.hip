@@ -17,6 +17,7 @@
 // address and are masked after the load (hipcc turns `c ? *p : 0` into a branch and a
 // full vmcnt(0) wait per element).
 #include "kernels.h"
+#include "lanes.h"
 #include "select.h"
 
 namespace mocr {
@@ -247,17 +248,8 @@ __device__ __forceinline__ void fold_tile(const FoldGemmParams& p, int c0) {
   if constexpr (YT) {
     const float y = rres + (val + p.by[gcol]);
     p.y[(size_t)grow * kD + gcol] = y;
-    float s = y;
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 4, 64);
-    s += __shfl_xor(s, 8, 64);
-    const float m16 = s * (1.0f / 16);
-    float q = (y - m16) * (y - m16);
-    q += __shfl_xor(q, 1, 64);
-    q += __shfl_xor(q, 2, 64);
-    q += __shfl_xor(q, 4, 64);
-    q += __shfl_xor(q, 8, 64);
+    const float m16 = row_sum<16>(y) * (1.0f / 16);  // the row's 16 lanes (DPP)
+    const float q = row_sum<16>((y - m16) * (y - m16));
     if (col == 0) {
       float* so = p.y_stats + ((size_t)grow * kSlices + c0 / 16) * 2;
       so[0] = m16;
@@ -384,15 +376,12 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
     s = fmaf(q4[1], kk[it][1], s);
     s = fmaf(q4[2], kk[it][2], s);
     s = fmaf(q4[3], kk[it][3], s);
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 4, 64);
+    s = row_sum<8>(s);  // the 8 lanes of the key row (DPP, as the xor butterfly)
     s *= kAttnScale;
     sc[it] = (m_first + it * 4 * RPW < n) ? s : -INFINITY;
     mx = fmaxf(mx, sc[it]);
   }
-#pragma unroll
-  for (int o = LPR; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  mx = xmax8_16_32(mx);  // over the wave's 8 key-row groups
   float sum = 0.f;
   floatx4 o4 = {0.f, 0.f, 0.f, 0.f};
   if (mx != -INFINITY) {
@@ -406,14 +395,9 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
       o4[3] = fmaf(e, vv[it][3], o4[3]);
     }
   }
+  sum = xsum8_16_32(sum);
 #pragma unroll
-  for (int o = LPR; o < 64; o <<= 1) {
-    sum += __shfl_xor(sum, o, 64);
-    o4[0] += __shfl_xor(o4[0], o, 64);
-    o4[1] += __shfl_xor(o4[1], o, 64);
-    o4[2] += __shfl_xor(o4[2], o, 64);
-    o4[3] += __shfl_xor(o4[3], o, 64);
-  }
+  for (int e = 0; e < 4; ++e) o4[e] = xsum8_16_32(o4[e]);
   if (rsub == 0) {
     po[wave][li] = o4;
     if (li == 0) {

@@ -19,6 +19,7 @@
 // no kernel reads device state before issuing its loads.  With the batch-global stop,
 // the stop flag is read alongside the loads and checked before the first store.
 #include "kernels.h"
+#include "lanes.h"
 #include "select.h"
 
 namespace mocr {
@@ -187,20 +188,21 @@ __global__ void __launch_bounds__(256) rowgemm_kernel(RowGemmParams p) {
     if (cv) p.out[(p.hist_stride ? (size_t)t * p.hist_stride : 0) + (size_t)grow * p.ldo + gcol] = v;
     if (p.part) {
       // the tile's (max, first argmax, sum exp(l - max)) over its 16 columns of the row
+      // over the row's 16 lanes by DPP (quad_perm xor 1, xor 2, row_half_mirror,
+      // row_mirror): the max with its first index is the same whichever lane pairs first
       float m = cv ? v : -INFINITY;
       int ix = gcol;
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        const float om = __shfl_xor(m, o, 64);
-        const int oi = __shfl_xor(ix, o, 64);
+      auto step = [&](float om, int oi) {
         if (om > m || (om == m && oi < ix)) {
           m = om;
           ix = oi;
         }
-      }
-      float e = cv ? expf(v - m) : 0.f;
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) e += __shfl_xor(e, o, 64);
+      };
+      step(dpp<0xB1>(m), __builtin_amdgcn_mov_dpp(ix, 0xB1, 0xF, 0xF, false));
+      step(dpp<0x4E>(m), __builtin_amdgcn_mov_dpp(ix, 0x4E, 0xF, 0xF, false));
+      step(dpp<0x141>(m), __builtin_amdgcn_mov_dpp(ix, 0x141, 0xF, 0xF, false));
+      step(dpp<0x140>(m), __builtin_amdgcn_mov_dpp(ix, 0x140, 0xF, 0xF, false));
+      const float e = row_sum<16>(cv ? expf(v - m) : 0.f);
       if (col == 0)
         reinterpret_cast<floatx4*>(p.part)[(size_t)grow * gridDim.x + blockIdx.x] = floatx4{m, __int_as_float(ix), e, 0.f};
     }
@@ -216,18 +218,9 @@ __global__ void __launch_bounds__(256) rowgemm_kernel(RowGemmParams p) {
   } else if constexpr (EPI == DEC_RESADD) {
     const float y = rres + v;
     p.out[(size_t)grow * p.ldo + gcol] = y;
-    // (mean, M2) of this row's 16-column slice, reduced over the 16 lanes of the row
-    float s = y;
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 4, 64);
-    s += __shfl_xor(s, 8, 64);
-    const float m16 = s * (1.0f / 16);
-    float q = (y - m16) * (y - m16);
-    q += __shfl_xor(q, 1, 64);
-    q += __shfl_xor(q, 2, 64);
-    q += __shfl_xor(q, 4, 64);
-    q += __shfl_xor(q, 8, 64);
+    // (mean, M2) of this row's 16-column slice, reduced over the 16 lanes of the row (DPP)
+    const float m16 = row_sum<16>(y) * (1.0f / 16);
+    const float q = row_sum<16>((y - m16) * (y - m16));
     if (col == 0) {
       float* so = p.out_stats + ((size_t)grow * kSlices + blockIdx.x) * 2;
       so[0] = m16;
@@ -345,15 +338,13 @@ __global__ void __launch_bounds__(256) dec_attn_kernel(const DecodeState* st, in
     s = fmaf(q4[1], kk[it][1], s);
     s = fmaf(q4[2], kk[it][2], s);
     s = fmaf(q4[3], kk[it][3], s);
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 4, 64);
+    s = row_sum<8>(s);
     s *= kAttnScale;
     sc[it] = (m_first + it * 4 * RPW < n) ? s : -INFINITY;
     mx = fmaxf(mx, sc[it]);
   }
-#pragma unroll
-  for (int o = LPR; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  static_assert(LPR == 8, "DPP reductions assume 8 lanes per key row");
+  mx = xmax8_16_32(mx);
   float sum = 0.f;
   floatx4 o4 = {0.f, 0.f, 0.f, 0.f};
   if (mx != -INFINITY) {
@@ -367,14 +358,9 @@ __global__ void __launch_bounds__(256) dec_attn_kernel(const DecodeState* st, in
       o4[3] = fmaf(e, vv[it][3], o4[3]);
     }
   }
+  sum = xsum8_16_32(sum);
 #pragma unroll
-  for (int o = LPR; o < 64; o <<= 1) {
-    sum += __shfl_xor(sum, o, 64);
-    o4[0] += __shfl_xor(o4[0], o, 64);
-    o4[1] += __shfl_xor(o4[1], o, 64);
-    o4[2] += __shfl_xor(o4[2], o, 64);
-    o4[3] += __shfl_xor(o4[3], o, 64);
-  }
+  for (int e = 0; e < 4; ++e) o4[e] = xsum8_16_32(o4[e]);
   if (rsub == 0) {
     po[wave][li] = o4;
     if ((li & 7) == 0) {
@@ -491,9 +477,7 @@ __global__ void __launch_bounds__(256, 3) dec_projattn_kernel(ProjAttnParams p) 
 #pragma unroll
   for (int pj = 0; pj < NP; ++pj) {
     float a = acc[pj];
-    a += __shfl_xor(a, 1, 64);
-    a += __shfl_xor(a, 2, 64);
-    a += __shfl_xor(a, 4, 64);
+    a = row_sum<8>(a);
     if (kc == 0) proj[pj][o] = a + p.bias[pj * kD + h * 32 + o];
   }
   __syncthreads();
@@ -531,16 +515,14 @@ __global__ void __launch_bounds__(256, 3) dec_projattn_kernel(ProjAttnParams p) 
       sv = fmaf(q4[1], kk[j][1], sv);
       sv = fmaf(q4[2], kk[j][2], sv);
       sv = fmaf(q4[3], kk[j][3], sv);
-      sv += __shfl_xor(sv, 1, 64);
-      sv += __shfl_xor(sv, 2, 64);
-      sv += __shfl_xor(sv, 4, 64);
+      sv = row_sum<8>(sv);
       sv *= kAttnScale;
       const int it = c * CH + j;
       sc[j] = (it < NIT && m_first + it * 4 * RPW < n) ? sv : -INFINITY;
       mc = fmaxf(mc, sc[j]);
     }
-#pragma unroll
-    for (int off = LPR; off < 64; off <<= 1) mc = fmaxf(mc, __shfl_xor(mc, off, 64));
+    static_assert(LPR == 8, "DPP reductions assume 8 lanes per key row");
+    mc = xmax8_16_32(mc);
     const float mnew = fmaxf(mrun, mc);
     if (mnew != -INFINITY) {
       const float scale = expf(mrun - mnew);
@@ -561,14 +543,9 @@ __global__ void __launch_bounds__(256, 3) dec_projattn_kernel(ProjAttnParams p) 
       mrun = mnew;
     }
   }
+  sum = xsum8_16_32(sum);
 #pragma unroll
-  for (int off = LPR; off < 64; off <<= 1) {
-    sum += __shfl_xor(sum, off, 64);
-    o4[0] += __shfl_xor(o4[0], off, 64);
-    o4[1] += __shfl_xor(o4[1], off, 64);
-    o4[2] += __shfl_xor(o4[2], off, 64);
-    o4[3] += __shfl_xor(o4[3], off, 64);
-  }
+  for (int e = 0; e < 4; ++e) o4[e] = xsum8_16_32(o4[e]);
   if (rsub == 0) {
     po[wave][li] = o4;
     if (li == 0) {

@@ -30,6 +30,7 @@
 // LN-partition kernel, the fp32 QKV round trip and the attention kernel's re-read
 // (s3, PMC: 864 MB -> 195 MB of HBM traffic per block before proj).
 #include "kernels.h"
+#include "lanes.h"
 
 namespace mocr {
 
@@ -54,63 +55,6 @@ __device__ __forceinline__ floatx4 mma(const bf16x8 (&a)[2], const bf16x8 (&b)[2
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], c, 0, 0, 0);
   }
   return c;
-}
-
-template <int CTRL>
-__device__ __forceinline__ float dpp(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
-}
-// sum over aligned groups of L lanes (L = 8, 16, 32): quad_perm xor 1, xor 2, then
-// row_half_mirror / row_mirror, which pair each lane with one of the other half's
-// lanes, all of which hold the same partial sum by then (== __shfl_xor by 4, 8), then
-// (L = 32) the other 16-lane row by v_permlane16_swap (as swap16 below)
-template <int L>
-__device__ __forceinline__ float row_sum(float s) {
-  static_assert(L == 8 || L == 16 || L == 32 || L == 64, "row_sum: 8, 16, 32 or 64 lanes");
-  s += dpp<0xB1>(s);
-  s += dpp<0x4E>(s);
-  s += dpp<0x141>(s);
-  if constexpr (L >= 16) s += dpp<0x140>(s);
-  if constexpr (L >= 32) {
-    float a = s, b = s;
-    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-    s = a + b;
-  }
-  if constexpr (L == 64) {
-    float a = s, b = s;
-    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-    s = a + b;
-  }
-  return s;
-}
-// x[lane ^ 16] and x[lane ^ 32] via v_permlane{16,32}_swap (VALU, no LDS queue).  The
-// swap exchanges halves between two registers, so both start as copies of x and their
-// sum / max is symmetric in the pair.  Inline asm: the builtin with one value for both
-// operands returned the same register twice (hardware-checked, tools/lane_ops_test.hip);
-// s_nop 1 covers the VALU-write -> permlane-read hazard.
-__device__ __forceinline__ void swap16(float& a, float& b) {
-  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-}
-__device__ __forceinline__ void swap32(float& a, float& b) {
-  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-}
-__device__ __forceinline__ float xmax16_32(float x) {
-  float a = x, b = x;
-  swap16(a, b);
-  x = fmaxf(a, b);
-  a = x;
-  b = x;
-  swap32(a, b);
-  return fmaxf(a, b);
-}
-__device__ __forceinline__ float xsum16_32(float x) {
-  float a = x, b = x;
-  swap16(a, b);
-  x = a + b;
-  a = x;
-  b = x;
-  swap32(a, b);
-  return a + b;
 }
 
 // 8 bf16 of row `row` (channels ch .. ch+7) of a [rows, C] plane pair
