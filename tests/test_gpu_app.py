@@ -43,3 +43,29 @@ def test_app_on_engine(pkg):
     assert [x["formula"] for x in body["results"]] == [s[0] for s in single]
     np.testing.assert_allclose([x["confidence"] for x in body["results"]], [s[1] for s in single], rtol=1e-6)
     eng.close()
+
+
+def test_load_model_checkpoint_file(pkg, golden, tmp_path):
+    """f2 on the GPU: a training checkpoint file ({'model_state_dict': ...} with the
+    encoder.swin.features.* aliases and the buffers the reference's state_dict holds,
+    src/utils.py:61-71) through im2latex.load_model (weights-only torch.load) decodes the
+    96x320 fixture batch to the reference's ids, batch-global stop included."""
+    import torch
+    from oracle.gen_golden import apply_eos_boost
+    g = golden("g96x320_b4_eos")
+    m = g["meta"]
+    w = apply_eos_boost(pkg.synth.make_weights(m["seed"], m["variant"]), m["eos_boost"])
+    sd = {}
+    for k, v in w.items():
+        sd[k] = torch.from_numpy(v)
+        if k.startswith("encoder.features."):  # the alias the reference's state_dict carries too
+            sd["encoder.swin." + k[len("encoder."):]] = torch.from_numpy(v)
+    sd["decoder.tgt_mask"] = torch.triu(torch.full((150, 150), float("-inf")), diagonal=1)
+    path = tmp_path / "best_model.pth"
+    torch.save({"epoch": 7, "model_state_dict": sd}, path)
+    vocab, _ = pkg.synth.synthetic_vocab()
+    eng = pkg.im2latex.load_model(str(path), vocab, "cuda:0", max_batch=m["B"], precision="fp32")
+    eng.encode(pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m["img_kind"]))
+    res = eng.decode(max_steps=m["steps"], stop="batch")
+    eng.close()
+    np.testing.assert_array_equal(res.ids, g["ids"])
