@@ -20,6 +20,7 @@
 // chunks of each row XOR-swizzled so the fragment reads are conflict-free),
 // double-buffered: chunk j+1 is loaded while chunk j runs, one barrier per chunk.
 #include "kernels.h"
+#include "lanes.h"
 
 namespace mocr {
 
@@ -182,8 +183,7 @@ __global__ void __launch_bounds__(512) mlp_fused_kernel(MlpParams p) {
     for (int ks = 0; ks < KS1; ++ks)
 #pragma unroll
       for (int e = 0; e < 8; ++e) s += v[ks][e];
-    s += __shfl_xor(s, 16, 64);
-    s += __shfl_xor(s, 32, 64);
+    s = xsum16_32(s);  // permlane swaps (lanes.h), the butterfly's pairs
     const float mean = s / (float)C;
     float q = 0.f;
 #pragma unroll
@@ -193,8 +193,7 @@ __global__ void __launch_bounds__(512) mlp_fused_kernel(MlpParams p) {
         const float d = v[ks][e] - mean;
         q += d * d;
       }
-    q += __shfl_xor(q, 16, 64);
-    q += __shfl_xor(q, 32, 64);
+    q = xsum16_32(q);
     const float rstd = 1.0f / sqrtf(q / (float)C + 1e-5f);
 #pragma unroll
     for (int ks = 0; ks < KS1; ++ks) {

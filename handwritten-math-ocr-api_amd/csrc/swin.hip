@@ -8,6 +8,7 @@
 // rows after LayerNorm, so their k/v equal the qkv bias and they stay unmasked keys,
 // exactly as in torchvision.
 #include "kernels.h"
+#include "lanes.h"
 
 namespace mocr {
 
@@ -112,8 +113,7 @@ __global__ void __launch_bounds__(256) ln_group_kernel(const float* __restrict__
     float s = 0.f;
 #pragma unroll
     for (int e = 0; e < F; ++e) s += v[e];
-#pragma unroll
-    for (int m = 1; m < LPR; m <<= 1) s += __shfl_xor(s, m, 64);
+    s = row_sum<LPR>(s);  // the row's LPR lanes, by DPP / permlane (lanes.h; the butterfly's pairs)
     const float mean = s / (float)geo.C;
     float q = 0.f;
 #pragma unroll
@@ -121,8 +121,7 @@ __global__ void __launch_bounds__(256) ln_group_kernel(const float* __restrict__
       const float d = v[e] - mean;
       q += d * d;
     }
-#pragma unroll
-    for (int m = 1; m < LPR; m <<= 1) q += __shfl_xor(q, m, 64);
+    q = row_sum<LPR>(q);
     const float rstd = 1.0f / sqrtf(q / (float)geo.C + 1e-5f);
 #pragma unroll
     for (int e = 0; e < F; e += 4) {
@@ -208,8 +207,7 @@ __global__ void __launch_bounds__(256) stem16_kernel(const float* __restrict__ i
       v[c] = acc + br[c];
       s += v[c];
     }
-#pragma unroll
-    for (int m = 1; m < 16; m <<= 1) s += __shfl_xor(s, m, 64);
+    s = row_sum<16>(s);  // the token's 16 lanes, by DPP (lanes.h; the xor butterfly's pairs)
     const float mean = s / 96.f;
     float q = 0.f;
 #pragma unroll
@@ -217,8 +215,7 @@ __global__ void __launch_bounds__(256) stem16_kernel(const float* __restrict__ i
       const float d = v[c] - mean;
       q += d * d;
     }
-#pragma unroll
-    for (int m = 1; m < 16; m <<= 1) q += __shfl_xor(q, m, 64);
+    q = row_sum<16>(q);
     const float rstd = 1.0f / sqrtf(q / 96.f + 1e-5f);
     float* dst = X + (size_t)tok * 96 + c0;
     float o[6];
@@ -505,8 +502,7 @@ __global__ void __launch_bounds__(256) window_attention_mfma_kernel(const float*
         m = fmaxf(m, st[kt][r]);
       }
     }
-    m = fmaxf(m, __shfl_xor(m, 16));
-    m = fmaxf(m, __shfl_xor(m, 32));
+    m = xmax16_32(m);
     float sum = 0.f;
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
@@ -515,8 +511,7 @@ __global__ void __launch_bounds__(256) window_attention_mfma_kernel(const float*
         st[kt][r] = expf(st[kt][r] - m);
         sum += st[kt][r];
       }
-    sum += __shfl_xor(sum, 16);
-    sum += __shfl_xor(sum, 32);
+    sum = xsum16_32(sum);
     abf16x8 ph[2], pl[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
