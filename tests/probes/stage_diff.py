@@ -1,0 +1,29 @@
+"""Debug aid (GPU): the fp32 / bf16x3 encoder maps after every features[k] of the smoke
+image with the given libmathocr.so, saved to OUT.npz (compare two builds bit for bit).
+    python tests/probes/stage_diff.py LIB OUT.npz
+"""
+import importlib
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401
+
+pkg = importlib.import_module("handwritten-math-ocr-api_amd")
+pkg.engine.load_library(sys.argv[1])
+w = pkg.synth.make_weights(5, "perturbed")
+img = pkg.synth.make_images(1, 96, 320, 1000, "ink")
+out = {}
+for prec in ("fp32", "bf16x3"):
+    eng = pkg.Engine(img_hw=(96, 320), max_batch=1, precision=prec, device=0)
+    eng.load_weights(w)
+    eng.encode(img)
+    shapes = [(1, 24, 80, 96)] * 2 + [(1, 12, 40, 192)] * 2 + [(1, 6, 20, 384)] * 2 + [(1, 3, 10, 768)] * 2
+    for k in range(8):
+        out[f"{prec}_{k}"] = eng.encode_until(k, shapes[k])
+    eng.encode(img)
+    out[f"{prec}_mem"] = eng.memory()
+    eng.close()
+np.savez(sys.argv[2], **out)
+print("saved", sys.argv[2])
