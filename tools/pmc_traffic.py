@@ -52,8 +52,14 @@ def main(fetch_csv, write_csv, out, decode_steps=0):
     afused = sorted({1 if "swin_attn_kernel<96" in k else 2 for k in kn if "swin_attn_kernel" in k})
     anoproj = [3] if any("swin_attn_noproj_kernel" in k for k in kn) else []
     names = classes_in_order(fused, afused, anoproj)
-    if not any("split_bf16" in k for k in kn[:3]):  # fp32 mode has no bf16 split kernels
-        names = [n for n in names if not n.startswith("split")]
+    # load-time bf16 splits before the stem: weights, kv-weights, and (bf16x3) the folded
+    # decoder weights; fp32 mode has none
+    n_split = next(i for i, k in enumerate(kn) if "stem" in k)
+    names = names[n_split - min(n_split, 2):] if n_split < 2 else names
+    if n_split == 0:
+        names = [n for n in names if not n.startswith("split(w") and not n.startswith("split(kv")]
+    elif n_split > 2:
+        names = names[:2] + [f"split(load {i})" for i in range(2, n_split)] + names[2:]
     n_enc = len(names)
     assert len(f) >= n_enc, (len(f), n_enc)
     if not decode_steps:
