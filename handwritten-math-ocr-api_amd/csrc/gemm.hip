@@ -1030,7 +1030,8 @@ bool try_big_tile(const GemmParams& p, hipStream_t s) {
 }
 
 // force_kernel values (tools/gemm_bench A/B; 0 = the dispatch's choice)
-enum : int { kKernelAuto = -1, kKernelStag = 1, kKernelBig = 2, kKernelTile = 3, kKernelQ288x256 = 10, kKernelQ288x192 = 11 };
+enum : int { kKernelAuto = -1, kKernelStag = 1, kKernelBig = 2, kKernelTile = 3, kKernelQ288x256 = 10, kKernelQ288x192 = 11,
+             kKernelQ288x128 = 12 };
 
 template <int PASSES>
 void launch_forced(const GemmParams& p, hipStream_t s) {
@@ -1056,6 +1057,9 @@ void launch_forced(const GemmParams& p, hipStream_t s) {
       break;
     case kKernelQ288x192:
       if (x3 && p.N % 192 == 0) return launch_stagq<9, 3, 3, 3>(p, s);
+      break;
+    case kKernelQ288x128:
+      if (x3 && p.N % 128 == 0) return launch_stagq<9, 2, 3, 2>(p, s);
       break;
   }
   throw std::runtime_error("gemm_bf16: forced kernel does not fit the shape");
