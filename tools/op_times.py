@@ -1,7 +1,7 @@
 """Per-op HIP-event times of one 64-image 384x384 encode (the engine's timed() names),
 fused vs unfused attention / MLP variants side by side.
 
-    python tools/op_times.py [--encodes 3] [--filter s3.,s4.]
+    python tools/op_times.py [--encodes 3] [--filter s3.,s4.] [--lib LIB]
 """
 import argparse
 import importlib
@@ -15,8 +15,11 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--encodes", type=int, default=3)
 ap.add_argument("--filter", default="")
 ap.add_argument("--variants", default="production,unfused_attn")
+ap.add_argument("--lib", default=None, help="libmathocr.so to load (an A/B build from tools/build_variant.sh)")
 a = ap.parse_args()
 pkg = importlib.import_module("handwritten-math-ocr-api_amd")
+if a.lib:
+    pkg.engine.load_library(a.lib)
 imgs = pkg.synth.make_images(64, 384, 384)
 w = pkg.synth.make_weights(1234, "init")
 res = {}
