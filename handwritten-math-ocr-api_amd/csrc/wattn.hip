@@ -226,6 +226,9 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
       pack8(x, kf[kt][0], kf[kt][1]);
     }
   }
+  // the three GEMMs one after the other: interleaved by the scheduler they spilled 72 B
+  // per lane at C = 96 (s1.attn 935 -> 890 us per block pair, profiles/r02/ab_s12_sched_barrier.log)
+  __builtin_amdgcn_sched_barrier(0);
   {
     // v [tokens x dims]: A = LN rows, B = W_v rows
     floatx4 acc[4][2];
@@ -259,6 +262,7 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
       }
     }
   }
+  __builtin_amdgcn_sched_barrier(0);
   {
     floatx4 acc[2][4];
     gemm_t(32 * h, acc);
