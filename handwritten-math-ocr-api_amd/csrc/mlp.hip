@@ -261,46 +261,87 @@ __global__ void __launch_bounds__(512) mlp_fused_kernel(MlpParams p) {
       }
     __builtin_amdgcn_s_setprio(0);
 
-    // bias + GELU; the accumulators of hidden tiles 2p, 2p+1 are GEMM 2's B fragment p
-    bf16x8 hb[KP][TT][PL];
+    if constexpr (C == 192) {
+      // bias + GELU of hidden tiles 2p, 2p+1 (GEMM 2's B fragment p) next to GEMM 2's k-step
+      // p, without a priority bracket, so the scheduler overlaps the GELU of p + 1 with the
+      // MFMAs of p: s2.mlp 793 -> 759 us per block pair; at C = 96 it measured 2.7 % slower
+      // (profiles/r02/ab_mlp_interleave.log)
 #pragma unroll
-    for (int kp = 0; kp < KP; ++kp)
-#pragma unroll
-      for (int tt = 0; tt < TT; ++tt) {
-        const float* bb = b1s + jc * NC + 32 * kp + 4 * g;
-        float h[8];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          h[r] = gelu_erf_fast(acc1[2 * kp][tt][r] + bb[r]);
-          h[4 + r] = gelu_erf_fast(acc1[2 * kp + 1][tt][r] + bb[16 + r]);
-        }
-        bf16x8 hi, lo;
-        pack8(h, hi, lo);
-        hb[kp][tt][0] = hi;
-        if constexpr (X3) hb[kp][tt][PL - 1] = lo;
-      }
-
-    // GEMM 2: out^T [C x 16TT] += W2[:, chunk] . hidden^T, k order as above
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kp = 0; kp < KP; ++kp)
-#pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) {
-        const int r = ct * 16 + j16;
-        const int o = r * (NC * 2) + ((4 * kp + g) ^ ((r >> SH2) & (RB - 1))) * 16;
-        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(w2s + o);
-        bf16x8 al = ah;
-        if constexpr (X3) al = *reinterpret_cast<const bf16x8*>(w2s + W2B + o);
+      for (int kp = 0; kp < KP; ++kp) {
+        bf16x8 hb[TT][PL];
 #pragma unroll
         for (int tt = 0; tt < TT; ++tt) {
-          acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hb[kp][tt][0], acc2[ct][tt], 0, 0, 0);
-          if constexpr (X3) {
-            acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hb[kp][tt][1], acc2[ct][tt], 0, 0, 0);
-            acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, hb[kp][tt][0], acc2[ct][tt], 0, 0, 0);
+          const float* bb = b1s + jc * NC + 32 * kp + 4 * g;
+          float h[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            h[r] = gelu_erf_fast(acc1[2 * kp][tt][r] + bb[r]);
+            h[4 + r] = gelu_erf_fast(acc1[2 * kp + 1][tt][r] + bb[16 + r]);
+          }
+          bf16x8 hi, lo;
+          pack8(h, hi, lo);
+          hb[tt][0] = hi;
+          if constexpr (X3) hb[tt][PL - 1] = lo;
+        }
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) {
+          const int r = ct * 16 + j16;
+          const int o = r * (NC * 2) + ((4 * kp + g) ^ ((r >> SH2) & (RB - 1))) * 16;
+          const bf16x8 ah = *reinterpret_cast<const bf16x8*>(w2s + o);
+          bf16x8 al = ah;
+          if constexpr (X3) al = *reinterpret_cast<const bf16x8*>(w2s + W2B + o);
+#pragma unroll
+          for (int tt = 0; tt < TT; ++tt) {
+            acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hb[tt][0], acc2[ct][tt], 0, 0, 0);
+            if constexpr (X3) {
+              acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hb[tt][1], acc2[ct][tt], 0, 0, 0);
+              acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, hb[tt][0], acc2[ct][tt], 0, 0, 0);
+            }
           }
         }
       }
-    __builtin_amdgcn_s_setprio(0);
+    } else {
+      // bias + GELU; the accumulators of hidden tiles 2p, 2p+1 are GEMM 2's B fragment p
+      bf16x8 hb[KP][TT][PL];
+#pragma unroll
+      for (int kp = 0; kp < KP; ++kp)
+#pragma unroll
+        for (int tt = 0; tt < TT; ++tt) {
+          const float* bb = b1s + jc * NC + 32 * kp + 4 * g;
+          float h[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            h[r] = gelu_erf_fast(acc1[2 * kp][tt][r] + bb[r]);
+            h[4 + r] = gelu_erf_fast(acc1[2 * kp + 1][tt][r] + bb[16 + r]);
+          }
+          bf16x8 hi, lo;
+          pack8(h, hi, lo);
+          hb[kp][tt][0] = hi;
+          if constexpr (X3) hb[kp][tt][PL - 1] = lo;
+        }
+
+      // GEMM 2: out^T [C x 16TT] += W2[:, chunk] . hidden^T, k order as above
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kp = 0; kp < KP; ++kp)
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) {
+          const int r = ct * 16 + j16;
+          const int o = r * (NC * 2) + ((4 * kp + g) ^ ((r >> SH2) & (RB - 1))) * 16;
+          const bf16x8 ah = *reinterpret_cast<const bf16x8*>(w2s + o);
+          bf16x8 al = ah;
+          if constexpr (X3) al = *reinterpret_cast<const bf16x8*>(w2s + W2B + o);
+#pragma unroll
+          for (int tt = 0; tt < TT; ++tt) {
+            acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hb[kp][tt][0], acc2[ct][tt], 0, 0, 0);
+            if constexpr (X3) {
+              acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hb[kp][tt][1], acc2[ct][tt], 0, 0, 0);
+              acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, hb[kp][tt][0], acc2[ct][tt], 0, 0, 0);
+            }
+          }
+        }
+      __builtin_amdgcn_s_setprio(0);
+    }
     // the other buffer was last read in chunk jc - 1, before the barrier that ended it
     if (more) {
       char* buf = lds + ((jc + 1) & 1) * BUF;
