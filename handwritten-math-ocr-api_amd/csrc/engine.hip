@@ -233,7 +233,7 @@ void check_config(const mocr_config& c) {
           c.precision == MOCR_PRECISION_BF16X3,
       "precision");
   req((c.variant & ~(MOCR_VARIANT_UNFUSED_ATTN | MOCR_VARIANT_UNFUSED_MLP | MOCR_VARIANT_DEC_UNFOLDED |
-                      MOCR_VARIANT_S4_FUSED_ATTN)) == 0,
+                      MOCR_VARIANT_S4_FUSED_ATTN | MOCR_VARIANT_WINDOW_ROWS)) == 0,
       "variant: unknown MOCR_VARIANT_* flag");
   req(c.sos_id >= 0 && c.sos_id < c.vocab && c.eos_id >= 0 && c.eos_id < c.vocab, "special ids");
 }
@@ -1115,6 +1115,21 @@ struct mocr_engine {
           ap.wg = wg;
           timed(attn_n[s], 6.0 * rows * C * C + 4.0 * rows * kWinTok * C, 4.0 * rows * C + (dwl ? 4.0 : 2.0) * 3.0 * C * C +
                 (dwl ? 4.0 : 2.0) * rows * C, [&] { launch_swin_attn_noproj(ap, stream); });
+          gemm(proj_n[s], opATT, wop(w.projw), W(w.projb), X, nullptr, nullptr, (int)rows, C, C, EPI_RESADD, nullptr,
+               rows);
+        } else if (b16 && !(cfg.variant & MOCR_VARIANT_WINDOW_ROWS)) {
+          // the image's tokens only (stage 4 at 384²: 144 of 196 window slots per image):
+          // norm1 and qkv in X's row order, the attention kernel maps window slots to pixels
+          // and takes the padded tokens' k / v from the qkv bias, O comes out in X's order,
+          // proj is a plain residual-add GEMM (bitwise the window-row sequence below)
+          timed(ln1_n[s], 0, 8.0 * rows * C,
+                [&] { launch_layernorm(X, W(w.n1w), W(w.n1b), xw32, XWh, XWl, (int)rows, C, stream); });
+          gemm(qkv_n[s], opXW, wop(w.qkvw), W(w.qkvb), QKV, nullptr, nullptr, (int)rows, 3 * C, C, EPI_STORE,
+               nullptr, rows);
+          timed(att_n[s], 4.0 * rows * kWinTok * C, 4.0 * (double)rows * 4 * C, [&] {
+            launch_window_attention(QKV, relbias[bi], relmask[bi], att32, ATTh, ATTl, B, C, g.heads, wg,
+                                    attn_passes(), stream, W(w.qkvb));
+          });
           gemm(proj_n[s], opATT, wop(w.projw), W(w.projb), X, nullptr, nullptr, (int)rows, C, C, EPI_RESADD, nullptr,
                rows);
         } else {

@@ -89,8 +89,11 @@ void launch_layernorm(const float* X, const float* g, const float* b, float* Y, 
 // relbias [heads,49,49] and the region mask computed in-kernel; 1 / 3: bf16 / bf16x3
 // MFMA with relmask [types][heads][64][64] (bias + shift mask + -inf key padding; 4
 // window types for shifted blocks, 1 otherwise).
+// bqkv != nullptr (MFMA kernels only): QKV / O rows are the image's tokens in X's order and
+// the padded tokens' k / v are synthesised from the qkv bias (see swin.hip)
 void launch_window_attention(const float* QKV, const float* relbias, const float* relmask, float* O, uint16_t* Oh,
-                             uint16_t* Ol, int B, int C, int heads, const WinGeom& wg, int passes, hipStream_t s);
+                             uint16_t* Ol, int B, int C, int heads, const WinGeom& wg, int passes, hipStream_t s,
+                             const float* bqkv = nullptr);
 
 // PatchMerging gather (x0,x1,x2,x3 with zero pad) + LayerNorm(4C) -> Y [B*Ho*Wo, 4C].
 void launch_merge_ln(const float* X, const float* g, const float* b, float* Y, uint16_t* Yh, uint16_t* Yl, int B,

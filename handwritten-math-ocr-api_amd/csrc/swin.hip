@@ -411,10 +411,17 @@ __device__ __forceinline__ floatx4 mfma3(const abf16x8& ah, const abf16x8& al, c
   return c;
 }
 
+// One wave per (window, head).  Window-token mode (bqkv == nullptr): QKV rows are the
+// window tokens (the partition LayerNorm's order, padded tokens included) and O goes to
+// the same rows.  Pixel mode (bqkv != nullptr): QKV and O rows are the image's tokens in
+// X's order; a window slot maps to its pixel through the shift roll, and a padded token's
+// k / v are the qkv bias (its LayerNorm'd input is zero, so W . 0 + b, bitwise), its
+// query is never written.  Both modes give the same bits for every real token.
 template <int PASSES>
 __global__ void __launch_bounds__(256) window_attention_mfma_kernel(const float* __restrict__ QKV,
                                                                     const float* __restrict__ table, RowOut out,
-                                                                    int C, int heads, long npairs, WinGeom wg) {
+                                                                    int C, int heads, long npairs, WinGeom wg,
+                                                                    const float* __restrict__ bqkv) {
   const int lane = threadIdx.x & 63;
   const long pair = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (pair >= npairs) return;  // whole wave; nothing below synchronises across waves
@@ -423,17 +430,35 @@ __global__ void __launch_bounds__(256) window_attention_mfma_kernel(const float*
   const int l15 = lane & 15;
   const int g = lane >> 4;
   const int C3 = 3 * C;
-  const float* base = QKV + (size_t)win_g * kWinTok * C3 + h * kHeadDim;
   const float scale = 0.17677669529663687f;  // 32 ** -0.5
+  const int win = (int)(win_g % wg.nWin);
+  const int wy = win / wg.nWx;
+  const int wx = win - wy * wg.nWx;
+  const bool pix = bqkv != nullptr;
+  // row of window slot `lane` (slot = lane; >= 0 real token, -1 padded token, -2 slot >= 49)
+  int slot_row;
+  {
+    const int ty = lane / kWin;
+    int y = wy * kWin + ty + wg.sh;
+    int x = wx * kWin + (lane - ty * kWin) + wg.sw;
+    if (y >= wg.pH) y -= wg.pH;
+    if (x >= wg.pW) x -= wg.pW;
+    const long b = win_g / wg.nWin;
+    slot_row = lane >= kWinTok ? -2 : (y < wg.H && x < wg.W ? (int)((b * wg.H + y) * wg.W + x) : -1);
+    if (!pix) slot_row = lane < kWinTok ? (int)(win_g * kWinTok + lane) : -2;
+  }
+  auto row_of = [&](int slot) { return __shfl(slot_row, slot); };
+  const float* base = QKV + h * kHeadDim;
 
   abf16x8 kh[4], kl[4];
 #pragma unroll
   for (int kt = 0; kt < 4; ++kt) {
-    const int key = 16 * kt + l15;
+    const int r = row_of(16 * kt + l15);
+    const float* src = r >= 0 ? base + (size_t)r * C3 + C + 8 * g : (r == -1 ? bqkv + C + h * kHeadDim + 8 * g : nullptr);
     float x[8];
-    if (key < kWinTok) {
-      const floatx4 a = *reinterpret_cast<const floatx4*>(base + (size_t)key * C3 + C + 8 * g);
-      const floatx4 b = *reinterpret_cast<const floatx4*>(base + (size_t)key * C3 + C + 8 * g + 4);
+    if (src) {
+      const floatx4 a = *reinterpret_cast<const floatx4*>(src);
+      const floatx4 b = *reinterpret_cast<const floatx4*>(src + 4);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         x[e] = a[e];
@@ -453,30 +478,27 @@ __global__ void __launch_bounds__(256) window_attention_mfma_kernel(const float*
       float x[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int key = 32 * s + (j >> 2) * 16 + 4 * g + (j & 3);
-        x[j] = key < kWinTok ? base[(size_t)key * C3 + 2 * C + 16 * dt + l15] : 0.f;
+        const int r = row_of(32 * s + (j >> 2) * 16 + 4 * g + (j & 3));
+        const int ch = 2 * C + 16 * dt + l15;
+        x[j] = r >= 0 ? base[(size_t)r * C3 + ch] : (r == -1 ? bqkv[h * kHeadDim + ch] : 0.f);
       }
       split8(x, vh[dt][s], vl[dt][s]);
     }
 
   int type = 0;
-  if (wg.sh + wg.sw > 0) {
-    const int win = (int)(win_g % wg.nWin);
-    const int wy = win / wg.nWx;
-    const int wx = win - wy * wg.nWx;
-    type = 2 * (wy == wg.nWin / wg.nWx - 1) + (wx == wg.nWx - 1);
-  }
+  if (wg.sh + wg.sw > 0) type = 2 * (wy == wg.nWin / wg.nWx - 1) + (wx == wg.nWx - 1);
   const float* tb = table + ((size_t)type * heads + h) * 64 * 64;
 
 #pragma unroll
   for (int qt = 0; qt < 4; ++qt) {
     const int q = 16 * qt + l15;
+    const int qr = row_of(q);
     abf16x8 qh, ql;
     {
       float x[8];
-      if (q < kWinTok) {
-        const floatx4 a = *reinterpret_cast<const floatx4*>(base + (size_t)q * C3 + 8 * g);
-        const floatx4 b = *reinterpret_cast<const floatx4*>(base + (size_t)q * C3 + 8 * g + 4);
+      if (qr >= 0) {
+        const floatx4 a = *reinterpret_cast<const floatx4*>(base + (size_t)qr * C3 + 8 * g);
+        const floatx4 b = *reinterpret_cast<const floatx4*>(base + (size_t)qr * C3 + 8 * g + 4);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           x[e] = a[e] * scale;
@@ -525,8 +547,8 @@ __global__ void __launch_bounds__(256) window_attention_mfma_kernel(const float*
       floatx4 o = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 2; ++s) o = mfma3<PASSES>(vh[dt][s], vl[dt][s], ph[s], pl[s], o);
-      if (q < kWinTok) {
-        const size_t off = ((size_t)win_g * kWinTok + q) * C + h * kHeadDim + 16 * dt + 4 * g;
+      if (qr >= 0) {
+        const size_t off = (size_t)qr * C + h * kHeadDim + 16 * dt + 4 * g;
         if (out.f32) *reinterpret_cast<floatx4*>(out.f32 + off) = o;
         if (out.hi) {
           uint32_t h0, l0, h1, l1;
@@ -590,7 +612,9 @@ void launch_merge_ln(const float* X, const float* g, const float* b, float* Y, u
 }
 
 void launch_window_attention(const float* QKV, const float* relbias, const float* relmask, float* O, uint16_t* Oh,
-                             uint16_t* Ol, int B, int C, int heads, const WinGeom& wg, int passes, hipStream_t s) {
+                             uint16_t* Ol, int B, int C, int heads, const WinGeom& wg, int passes, hipStream_t s,
+                             const float* bqkv) {
+  if (bqkv && passes == 0) throw std::runtime_error("window_attention: pixel-order rows need the MFMA kernel");
   if (passes == 0) {
     dim3 grid((unsigned)((long)B * wg.nWin), (unsigned)heads);
     window_attention_kernel<<<grid, 256, 0, s>>>(QKV, relbias, RowOut{O, Oh, Ol}, C, wg);
@@ -598,9 +622,9 @@ void launch_window_attention(const float* QKV, const float* relbias, const float
     const long npairs = (long)B * wg.nWin * heads;
     const unsigned blocks = (unsigned)((npairs + 3) / 4);
     if (passes == 3)
-      window_attention_mfma_kernel<3><<<blocks, 256, 0, s>>>(QKV, relmask, RowOut{O, Oh, Ol}, C, heads, npairs, wg);
+      window_attention_mfma_kernel<3><<<blocks, 256, 0, s>>>(QKV, relmask, RowOut{O, Oh, Ol}, C, heads, npairs, wg, bqkv);
     else if (passes == 1)
-      window_attention_mfma_kernel<1><<<blocks, 256, 0, s>>>(QKV, relmask, RowOut{O, Oh, Ol}, C, heads, npairs, wg);
+      window_attention_mfma_kernel<1><<<blocks, 256, 0, s>>>(QKV, relmask, RowOut{O, Oh, Ol}, C, heads, npairs, wg, bqkv);
     else
       throw std::runtime_error("window_attention: passes must be 0, 1 or 3");
   }

@@ -25,7 +25,7 @@ STOP = {"batch": 0, "none": 1}
 ARCH = {"swin": 0, "res18trans": 1}
 ABI_VERSION = 4
 # kernel-path variants (include/mathocr.h MOCR_VARIANT_*): 0 = production
-VARIANT = {"unfused_attn": 1, "unfused_mlp": 2, "dec_unfolded": 4, "s4_fused_attn": 8}
+VARIANT = {"unfused_attn": 1, "unfused_mlp": 2, "dec_unfolded": 4, "s4_fused_attn": 8, "window_rows": 16}
 
 
 class MocrConfig(ctypes.Structure):

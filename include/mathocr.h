@@ -71,9 +71,12 @@ enum {
   MOCR_VARIANT_UNFUSED_MLP = 2,  /* Swin stages 1-2: LN, fc1, fc2 instead of mlp.hip's fused kernel */
   MOCR_VARIANT_DEC_UNFOLDED = 4, /* greedy decoder on the 8-kernel step (LayerNorms applied by their */
                                  /* consumers) instead of the folded 5-kernel step (decfold.hip)     */
-  MOCR_VARIANT_S4_FUSED_ATTN = 8 /* Swin stage 4 (C = 768): norm1 + qkv + W-MSA in one kernel (two   */
-                                 /* 384-channel LDS halves) -- measured slower than the unfused      */
-                                 /* sequence at 384x384, so off in production                        */
+  MOCR_VARIANT_S4_FUSED_ATTN = 8, /* Swin stage 4 (C = 768): norm1 + qkv + W-MSA in one kernel (two  */
+                                  /* 384-channel LDS halves) -- measured slower than the unfused     */
+                                  /* sequence at 384x384, so off in production                       */
+  MOCR_VARIANT_WINDOW_ROWS = 16   /* unfused Swin attention (stage 4, or with UNFUSED_ATTN) over the */
+                                  /* partitioned window rows, padded tokens included, instead of the */
+                                  /* image's tokens in pixel order                                   */
 };
 
 /* Greedy stopping rule (src/inference.py:23-25). */

@@ -50,7 +50,8 @@ def test_encoder_stages_match_oracle(pkg, g384):
         assert e < 1e-4, f"features[{k}] rel err {e}"
 
 
-@pytest.mark.parametrize("variant", [(), ("unfused_attn",), ("unfused_attn", "unfused_mlp"), ("s4_fused_attn",)])
+@pytest.mark.parametrize("variant", [(), ("unfused_attn",), ("unfused_attn", "unfused_mlp"), ("s4_fused_attn",),
+                                     ("window_rows",), ("unfused_attn", "window_rows")])
 def test_bf16x3_encoder_stages_match_oracle(pkg, golden, variant):
     """bf16x3 encoder stage by stage: the fused stage-1/2 attention half (wattn.hip) and
     MLP half (mlp.hip), the stage-3 no-proj kernel, the stage-4 two-half kernel (off in
@@ -68,6 +69,26 @@ def test_bf16x3_encoder_stages_match_oracle(pkg, golden, variant):
         e = rel_err(got, ref.numpy())
         assert e < 1e-4, f"features[{k}] rel err {e}"
     eng.close()
+
+
+@pytest.mark.parametrize("case,base", [("g384_b2_pert", ()), ("g384_b2_pert", ("unfused_attn",)),
+                                       ("g96x320_b4_eos", ("unfused_attn",))])
+def test_pixel_rows_bitwise_window_rows(pkg, golden, case, base):
+    """The unfused window attention over the image's tokens (production: stage 4; with
+    unfused_attn: every stage) against the same sequence over the partitioned window rows
+    (MOCR_VARIANT_WINDOW_ROWS): the padded tokens' k / v taken from the qkv bias must give
+    the same bits as the qkv GEMM of their zero LayerNorm rows, so the encoder memory is
+    bitwise equal (96x320: padding on both axes at every stage, shifted windows)."""
+    g = golden(case)
+    m = g["meta"]
+    imgs = pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m["img_kind"])
+    mem = []
+    for variant in (base, base + ("window_rows",)):
+        eng, _ = make_engine(pkg, m, precision="bf16x3", variant=variant)
+        eng.encode(imgs)
+        mem.append(eng.memory())
+        eng.close()
+    assert np.array_equal(mem[0].view(np.uint32), mem[1].view(np.uint32))
 
 
 def test_memory_matches_golden(pkg, g384):
