@@ -176,7 +176,11 @@ __global__ void __launch_bounds__(256) stem16_kernel(const float* __restrict__ i
 #pragma unroll
   for (int c = 0; c < 6; ++c) {
 #pragma unroll
-    for (int k = 0; k < 16; ++k) wr[c][k] = w[(c0 + c) * 16 + k];
+    for (int k4 = 0; k4 < 4; ++k4) {  // a channel's 16 weights as 4 float4
+      const floatx4 t = *reinterpret_cast<const floatx4*>(w + (c0 + c) * 16 + 4 * k4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wr[c][4 * k4 + e] = t[e];
+    }
     br[c] = bias[c0 + c];
     gr[c] = g[c0 + c];
     be[c] = beta[c0 + c];
@@ -577,7 +581,9 @@ void launch_stem(const float* img, const float* w, const float* b, const float* 
   const int Hs = H / 4, Ws = W / 4;
   if (W % 4 != 0) throw std::runtime_error("stem: image width must be a multiple of 4");
   const long ntok = (long)B * Hs * Ws;
-  const unsigned blocks = (unsigned)std::min<long>((ntok + 15) / 16, 4096);
+  // 1024 workgroups (9 tokens per wave at B = 64, 384²): 121 -> 111 us against 4096, whose
+  // waves paid the weight prologue for 2-3 tokens each (profiles/r02/ab_stem_grid.log)
+  const unsigned blocks = (unsigned)std::min<long>((ntok + 15) / 16, 1024);
   stem16_kernel<<<blocks, 256, 0, s>>>(img, w, b, ln_w, ln_b, X, ntok, H, W, Hs, Ws);
   MOCR_HIP_CHECK(hipGetLastError());
 }
