@@ -316,6 +316,8 @@ struct mocr_engine {
   int32_t *ids = nullptr, *feed = nullptr, *forced = nullptr, *finished = nullptr;
   float* logp = nullptr;
   DecodeState* st = nullptr;
+  DecodeState* st_host = nullptr;          // pinned, 2 slots: the state after alternate chunks
+  hipEvent_t chunk_ev[2] = {nullptr, nullptr};
   int ld_ids = 0;
   const SelectArgs* sel_prev = nullptr;  // record_step -> record_layers_fold (layer 0 of step t >= 1)
   int max_rows = 0;  // decoder rows the buffers hold: max_batch * max(1, max_beam)
@@ -350,6 +352,9 @@ struct mocr_engine {
     (void)hipSetDevice(device);
     for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
     for (auto e : event_pool) (void)hipEventDestroy(e);
+    for (auto e : chunk_ev)
+      if (e) (void)hipEventDestroy(e);
+    if (st_host) (void)hipHostFree(st_host);
     for (auto& r : pending) {
       (void)hipEventDestroy(r.e0);
       (void)hipEventDestroy(r.e1);
@@ -787,6 +792,8 @@ struct mocr_engine {
     finished = dalloc<int32_t>(B);
     logp = dalloc<float>(B * cfg.max_pos);
     st = dalloc<DecodeState>(1);
+    MOCR_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&st_host), 2 * sizeof(DecodeState), hipHostMallocDefault));
+    for (auto& e : chunk_ev) MOCR_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
 
   // [type][h][64 q][64 key] table of the bf16 attention kernel: bias[h][q][key] plus the
@@ -1552,6 +1559,9 @@ struct mocr_engine {
       t0 = get_event();
       MOCR_HIP_CHECK(hipEventRecord(t0, stream));
     }
+    // Batch stop: the state after chunk c is copied to a pinned slot behind chunk c, and
+    // the host checks chunk c - 1's copy only once chunk c is queued, so the GPU never
+    // idles between chunks; a chunk launched after the stop skips every step (dec_skip).
     for (int c = 0; c < chunks; ++c) {
       hipGraphExec_t ge = graph_for(B, c, max_steps, want_logits, forced_host != nullptr, stop_batch);
       const auto h0 = std::chrono::steady_clock::now();
@@ -1563,9 +1573,12 @@ struct mocr_engine {
         hs_.total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
       }
       if (stop_batch && c + 1 < chunks) {
-        MOCR_HIP_CHECK(hipMemcpyAsync(&hs, st, sizeof(hs), hipMemcpyDeviceToHost, stream));
-        MOCR_HIP_CHECK(hipStreamSynchronize(stream));
-        if (hs.done_step != 0x7fffffff) break;
+        MOCR_HIP_CHECK(hipMemcpyAsync(&st_host[c & 1], st, sizeof(DecodeState), hipMemcpyDeviceToHost, stream));
+        MOCR_HIP_CHECK(hipEventRecord(chunk_ev[c & 1], stream));
+        if (c > 0) {
+          MOCR_HIP_CHECK(hipEventSynchronize(chunk_ev[(c - 1) & 1]));
+          if (st_host[(c - 1) & 1].done_step != 0x7fffffff) break;
+        }
       }
     }
     MOCR_HIP_CHECK(hipMemcpyAsync(&hs, st, sizeof(hs), hipMemcpyDeviceToHost, stream));
