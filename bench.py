@@ -39,8 +39,9 @@ DTYPE = {"fp32": "f32", "bf16x3": "bf16x3", "bf16": "bf16"}
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=24,
-                    help="timed batches per GPU (the replica pipeline's fill and drain are inside the timed region)")
+    ap.add_argument("--steps", type=int, default=64,
+                    help="timed batches per GPU (the replica pipeline's fill and drain are inside the timed "
+                         "region: 64 batches read 0.8 %% above 24, profiles/r02/bench_steps_probe.log)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=64, help="images per batch (per GPU)")
     ap.add_argument("--image", type=int, nargs=2, default=[384, 384])
