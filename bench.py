@@ -121,20 +121,25 @@ def pmc_traffic(precision, cls):
         return None
 
 
-def roofline(stats, dtype, precision):
-    """Dominant encoder GEMM class by event-timed GPU time: algorithmic FLOP per launch /
-    average launch duration, against the dense bf16 MFMA peak (fp32 MFMA in fp32 mode).
-    bf16x3 issues three bf16 MFMAs per product (hi*hi + hi*lo + lo*hi), so the MFMA issue
-    rate is 3x the algorithmic rate: reported beside it as mfma_issue_frac."""
+def roofline(stats, dtype, precision, attention=False):
+    """Dominant encoder GEMM class (attention=False) or window-attention class
+    (attention=True: the fused norm1 + qkv + W-MSA kernels, s3.attn at 384²) by
+    event-timed GPU time: algorithmic FLOP per launch / average launch duration, against
+    the dense bf16 MFMA peak (fp32 MFMA in fp32 mode).  bf16x3 issues three bf16 MFMAs per
+    product (hi*hi + hi*lo + lo*hi), so the MFMA issue rate is 3x the algorithmic rate:
+    reported beside it as mfma_issue_frac."""
     gemms = {k: v for k, v in stats.items()
-             if v["flops"] > 0 and "attn" not in k and not k.endswith("stem") and k != "r.enc"
+             if v["flops"] > 0 and ("attn" in k) == attention and not k.endswith("stem") and k != "r.enc"
              and not k.startswith("decode")}
+    if not gemms:
+        return None
     name, d = max(gemms.items(), key=lambda kv: kv[1]["total_ms"])
     avg_ms = d["total_ms"] / d["launches"]
     flops = d["flops"] / d["launches"]
     achieved = flops / (avg_ms * 1e-3) / 1e12
     peak = PEAK[dtype]
-    out = {"kernel": f"gemm_{'f32' if dtype == 'f32' else 'bf16'}[{dtype}] {name}", "bound": "mfma",
+    kind = "attention" if attention else f"gemm_{'f32' if dtype == 'f32' else 'bf16'}"
+    out = {"kernel": f"{kind}[{dtype}] {name}", "bound": "mfma",
            "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
            "traffic": pmc_traffic(precision, name),
            "avg_launch_ms": avg_ms, "flops_per_launch": flops,
@@ -303,6 +308,9 @@ def main():
         out["p50_image_latency_unloaded_ms"] = iso["batch_latency_ms"]
         out["p50_image_latency_b1_ms"] = iso["b1_latency_ms"]
         out["roofline"] = roofline(iso["stats"], dtype, args.precision)
+        ra = roofline(iso["stats"], dtype, args.precision, attention=True)
+        if ra:
+            out["roofline_attention"] = ra
         rd = roofline_decode(iso["stats"], args.precision)
         if rd:
             out["roofline_decode"] = rd

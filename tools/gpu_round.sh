@@ -27,6 +27,8 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
   || { echo "ROCPROF FAILED"; tail -20 $O/prof_bench.log; exit 1; }
 python3 tools/trace_phase_stats.py $O/prof_bench/run_kernel_trace.csv "gemm_x3_stagq_kernel<1, 9, 4, 3, 2>" 6 \
   --json $O/trace_iso_s3fc1.json > /dev/null || echo "trace phase stats failed"
+python3 tools/trace_phase_stats.py $O/prof_bench/run_kernel_trace.csv "swin_attn_noproj_kernel<384, 3, 3, 12, 2>" 6 \
+  --json $O/trace_iso_s3attn.json > /dev/null || echo "trace phase stats failed"
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o run -- \
   python3 tools/profile_encoder.py --decode-steps 8 > $O/pmc_f.log 2>&1 || { echo "PMC F FAILED"; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o run -- \
