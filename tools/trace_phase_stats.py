@@ -8,6 +8,7 @@ of the run, the loaded ones included, so it reads higher under contention.  This
 takes the dispatches of the last `--iso-batches` batches of one kernel (the isolated
 phase; bench.py runs 3) and prints their statistics beside the whole-run ones, so the
 HIP-event average can be checked against the profiler's clock for the same dispatches.
+Only the kernel's full-batch dispatches (its largest grid) are counted.
 
 usage: tools/trace_phase_stats.py TRACE.csv KERNEL_SUBSTRING PER_BATCH [--iso-batches 3] [--json OUT]
 """
@@ -29,7 +30,13 @@ def main():
     with open(a.trace) as f:
         for r in csv.DictReader(f):
             if a.kernel in r["Kernel_Name"]:
-                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
+                             int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])))
+    # the bench's B = 1 latency engine runs after the isolated phase and may use the same
+    # kernel on a smaller grid: keep the full-batch dispatches (the largest grid)
+    if rows:
+        big = max(r[3] for r in rows)
+        rows = [r[:3] for r in rows if r[3] == big]
     rows.sort()
     if not rows:
         raise SystemExit(f"no dispatch of {a.kernel!r}")
