@@ -1,0 +1,73 @@
+"""CPU checks of bench.py's measurement helpers: the roofline lines are
+computed from HIP-event kernel-class records exactly as documented in DESIGN.md §5, and
+the committed PMC traffic profile maps to the kernel classes they name."""
+import importlib.util
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("bench_under_test", os.path.join(REPO, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def rec(launches, ms, flops, byts=0.0):
+    return {"launches": launches, "total_ms": ms * launches, "flops": flops * launches, "bytes": byts * launches}
+
+
+def stats():
+    # per-launch: s3.fc1 162 us / 43.5 GF, s3.fc2 153 us / 43.5 GF, s3.attn 286 us / 35.4 GF
+    return {
+        "s3.fc1": rec(18, 0.162, 43.486543872e9, 285.5e6),
+        "s3.fc2": rec(18, 0.153, 43.486543872e9),
+        "s3.attn": rec(18, 0.286, 35.38944e9, 115.0e6),
+        "s1.attn": rec(6, 0.465, 20.0e9),
+        "stem": rec(3, 0.114, 1.0e9),
+        "decode.greedy": rec(384, 0.2435, 0.95e9, 247.1e6),
+        "host.graph_launch": rec(48, 0.11, 0.0),
+    }
+
+
+def test_gemm_roofline_is_the_dominant_gemm_class(bench):
+    r = bench.roofline(stats(), "bf16x3", "bf16x3")
+    assert r["kernel"] == "gemm_bf16[bf16x3] s3.fc1" and r["bound"] == "mfma" and r["unit"] == "TFLOP/s"
+    assert r["achieved"] == pytest.approx(43.486543872e9 / 162e-6 / 1e12)
+    assert r["peak"] == 2500.0 and r["frac"] == pytest.approx(r["achieved"] / 2500.0)
+    assert r["mfma_issue_frac"] == pytest.approx(3 * r["frac"])
+    assert r["avg_launch_ms"] == pytest.approx(0.162)
+
+
+def test_attention_roofline_is_the_dominant_attention_class(bench):
+    r = bench.roofline(stats(), "bf16x3", "bf16x3", attention=True)
+    assert r["kernel"] == "attention[bf16x3] s3.attn"
+    assert r["achieved"] == pytest.approx(35.38944e9 / 286e-6 / 1e12)
+    assert bench.roofline({"s3.fc1": rec(1, 0.1, 1e9)}, "bf16x3", "bf16x3", attention=True) is None
+
+
+def test_decode_roofline_against_hbm(bench):
+    r = bench.roofline_decode(stats(), "bf16x3")
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert r["achieved"] == pytest.approx(247.1e6 / 0.2435e-3 / 1e9)
+    assert r["frac"] == pytest.approx(r["achieved"] / 8000.0)
+    assert bench.roofline_decode({}, "bf16x3") is None
+
+
+def test_committed_pmc_traffic_covers_the_roofline_classes(bench):
+    for cls in ("s3.fc1", "s3.attn", "decode.step"):
+        t = bench.pmc_traffic("bf16x3", cls)
+        assert t is not None and t > 0, cls
+    assert bench.pmc_traffic("bf16x3", "no.such.class") is None
+
+
+def test_default_run_is_one_gpu_minutes_scale(bench, monkeypatch):
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = bench.parse()
+    assert a.gpus == 1 and a.steps == 64 and a.warmup == 3 and a.batch == 64 and a.tokens == 128
+    assert a.replicas == 4 and a.precision == "bf16x3" and a.image == [384, 384]
