@@ -434,7 +434,11 @@ __global__ void __launch_bounds__(256, 3) dec_projattn_kernel(ProjAttnParams p) 
       const int it = c * CH + j;
       const int m = m_first + it * 4 * RPW;
       if (it < NIT && m < p.n_cached) {
-        const size_t r = slots ? (size_t)slots[m] : fixed_row;
+        // the slot tables of steps after a beam-search batch stop are not maintained (the
+        // selection skips), but this step's loads are issued before the skip is read:
+        // clamp the slot to a valid row so a stale entry cannot address past the cache
+        const int sl = slots ? slots[m] : 0;
+        const size_t r = slots ? (size_t)((unsigned)sl < (unsigned)p.B ? sl : 0) : fixed_row;
         kk[j] = *reinterpret_cast<const floatx4*>(Kh + r * p.kv_b_stride + (size_t)m * p.kv_row_stride);
         vv[j] = *reinterpret_cast<const floatx4*>(Vh + r * p.kv_b_stride + (size_t)m * p.kv_row_stride);
       } else {

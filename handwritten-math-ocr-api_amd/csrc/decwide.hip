@@ -1,0 +1,490 @@
+// Wide-tile fold GEMM of the greedy decode step (kernels.h FoldGemmParams) for decode
+// chains of 64-256+ rows: the same folded LayerNorm algebra as decfold.hip foldgemm_kernel
+// (torch/nn/modules/transformer.py:1143-1199 post-norm layer, see decfold.hip's header),
+// and the fc_out logits (src/model_swin.py:87) with the greedy selection's tile partials.
+//
+// decfold.hip computes 16x16 output tiles, so at R rows every tile re-reads its 16 A rows
+// and 16 W columns over the whole K from L2: at R = 256 the FFN fold GEMM (N = 1024,
+// K = 768) moves ~150 MB through L2 per launch for 0.2 GFLOP and takes 17 us
+// (profiles/r03/chain1).  Here a workgroup owns a BM x BN tile (32 x 32 at R > 64), its 4
+// waves split K four ways (each wave holds the whole tile's accumulators for its K range,
+// so A and W are each loaded once per workgroup) and combine through LDS in a fixed
+// order; loads run PD k-steps ahead of the MFMAs.  Blocks are numbered column tile
+// fastest, so block b's column tile is b mod ncol and, with ncol a multiple of 8, each
+// XCD (blocks b, b + 8, ...) streams 1/8 of W for every row tile.
+//
+// Columns [0, NY) are y tiles (K = K1 over A1'); columns [NY, NY + NZ) are z tiles over
+// [A1' | A2'] (K = K1 + d), as foldgemm_kernel.  LOGITS (K1 = 0, NY = 0): the z tiles are
+// fc_out over LN(A2), written to the logits slot of step t with the per-16-column
+// (max, first argmax, sum exp) partials the selection reads (decoder.hip DEC_LOGITS).
+#include "kernels.h"
+#include "lanes.h"
+
+namespace mocr {
+
+namespace {
+
+constexpr int kD = 256;
+constexpr int kSlices = kD / 16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split8(const floatx4& x0, const floatx4& x1, bf16x8& hi, bf16x8& lo) {
+  uint32_t h[4], l[4];
+  split2_bf16(x0[0], x0[1], h[0], l[0]);
+  split2_bf16(x0[2], x0[3], h[1], l[1]);
+  split2_bf16(x1[0], x1[1], h[2], l[2]);
+  split2_bf16(x1[2], x1[3], h[3], l[3]);
+  hi = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
+  lo = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
+}
+
+// Row statistics from the 16 (mean, M2) slice partials, merged by decoder.hip's fixed
+// binary tree (bit-identical to every other consumer of the same LayerNorm).
+__device__ __forceinline__ void merge_eq(float& m, float& q, float mb, float qb, float n) {
+  const float delta = mb - m;
+  q = q + qb + delta * delta * (n * 0.5f);
+  m = m + delta * 0.5f;
+}
+__device__ __forceinline__ void merge_lanes(float& m, float& q, int mask, bool upper, float n) {
+  const float mo = __shfl_xor(m, mask, 64);
+  const float qo = __shfl_xor(q, mask, 64);
+  if (upper) {
+    float mm = mo, qq = qo;
+    merge_eq(mm, qq, m, q, n);
+    m = mm;
+    q = qq;
+  } else {
+    merge_eq(m, q, mo, qo, n);
+  }
+}
+__device__ __forceinline__ float rstd_of(float m2) { return 1.0f / sqrtf(m2 * (1.0f / kD) + 1e-5f); }
+struct Part4 {
+  floatx4 p0, p1;
+};
+// layout 1: the 4 lanes g = 0..3 of a row (lane, lane ^ 16, ^ 32, ^ 48) hold slices 4g..4g+3
+__device__ __forceinline__ Part4 load_part4(const float* __restrict__ part, int g) {
+  return {*reinterpret_cast<const floatx4*>(part + 8 * g), *reinterpret_cast<const floatx4*>(part + 8 * g + 4)};
+}
+__device__ __forceinline__ void merge_part4(const Part4& pp, int g, float& mean, float& rstd) {
+  float m = pp.p0[0], q = pp.p0[1], m2 = pp.p1[0], q2 = pp.p1[1];
+  merge_eq(m, q, pp.p0[2], pp.p0[3], 16.f);
+  merge_eq(m2, q2, pp.p1[2], pp.p1[3], 16.f);
+  merge_eq(m, q, m2, q2, 32.f);
+  merge_lanes(m, q, 16, (g & 1) != 0, 64.f);
+  merge_lanes(m, q, 32, (g & 2) != 0, 128.f);
+  mean = m;
+  rstd = rstd_of(q);
+}
+// the same tree with the 4 lanes of a row adjacent (lane ^ 1, lane ^ 2: coalesced layout)
+__device__ __forceinline__ void merge_part4_quad(const Part4& pp, int g, float& mean, float& rstd) {
+  float m = pp.p0[0], q = pp.p0[1], m2 = pp.p1[0], q2 = pp.p1[1];
+  merge_eq(m, q, pp.p0[2], pp.p0[3], 16.f);
+  merge_eq(m2, q2, pp.p1[2], pp.p1[3], 16.f);
+  merge_eq(m, q, m2, q2, 32.f);
+  merge_lanes(m, q, 1, (g & 1) != 0, 64.f);
+  merge_lanes(m, q, 2, (g & 2) != 0, 128.f);
+  mean = m;
+  rstd = rstd_of(q);
+}
+// layout 2 from preloaded (mean, M2) of slice c
+__device__ __forceinline__ void row_stats_16lanes_v(float m, float q, int c, float& mean, float& rstd) {
+  merge_lanes(m, q, 1, (c & 1) != 0, 16.f);
+  merge_lanes(m, q, 2, (c & 2) != 0, 32.f);
+  merge_lanes(m, q, 4, (c & 4) != 0, 64.f);
+  merge_lanes(m, q, 8, (c & 8) != 0, 128.f);
+  mean = m;
+  rstd = rstd_of(q);
+}
+// layout 2: the 16 lanes c = 0..15 of a row each hold slice c
+__device__ __forceinline__ void row_stats_16lanes(const float* __restrict__ part, int c, float& mean, float& rstd) {
+  float m = part[2 * c], q = part[2 * c + 1];
+  merge_lanes(m, q, 1, (c & 1) != 0, 16.f);
+  merge_lanes(m, q, 2, (c & 2) != 0, 32.f);
+  merge_lanes(m, q, 4, (c & 4) != 0, 64.f);
+  merge_lanes(m, q, 8, (c & 8) != 0, 128.f);
+  mean = m;
+  rstd = rstd_of(q);
+}
+
+// LDS of one tile: the k-vectors (u, v), each wave's transformed A fragments, the 4-wave
+// reduction.  X3: per (k step, row fragment) a hi and a lo 1-KB fragment; fp32: one.
+template <int BM, int BN, bool YT, int K1, bool X3>
+struct TileLds {
+  static constexpr int KT = YT ? K1 : K1 + kD;
+  static constexpr int KW = KT / 4;
+  static constexpr int UV = 2 * KT * 4;
+  static constexpr int AW = (BM / 16) * (KW / (X3 ? 32 : 16)) * (X3 ? 2 : 1) * 1024;  // per wave
+  static constexpr int RED = 4 * BM * (BN + 1) * 4;
+  static constexpr int BYTES = UV + 4 * AW + RED;
+};
+
+// One BM x BN tile.  KT = the tile's K (K1 for y tiles, K1 + d for z tiles); each of the
+// 4 waves takes KT / 4 consecutive k.
+//  - A is loaded coalesced (lane = row (lane >> 2) x 16 bytes (lane & 3) of a 64-byte row
+//    segment, so every quad of lanes reads one segment), transformed once (FFN unfold +
+//    ReLU, LayerNorm), split into bf16 hi / lo (X3) and written to the wave's LDS region in
+//    MFMA fragment order; the k loop reads each fragment with one ds_read_b128.
+//  - W comes fragment-major (launch_frag_pack): one contiguous 1-KB load per 16-column x
+//    k-step fragment and plane.
+//  - Everything the epilogue reads (bias, LayerNorm vectors and statistics, residual) is
+//    loaded before the first store: a load issued after a store waits for it (vmcnt).
+// MFMA operands (16x16x32 bf16, or 16x16x4 f32 in four steps): row / column = lane & 15,
+// k = 8 g .. 8 g + 7 of the step (X3) or 4 g .. 4 g + 3 (fp32), g = lane >> 4.
+template <int BM, int BN, bool YT, int K1, bool S1, bool S2, bool X3, bool LOGITS>
+__device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c0, char* smem) {
+  using L = TileLds<BM, BN, YT, K1, X3>;
+  constexpr int MF = BM / 16, NF = BN / 16;
+  constexpr int KT = L::KT;
+  constexpr int KW = L::KW;
+  constexpr int KS = X3 ? 32 : 16;
+  constexpr int NKS = KW / KS;
+  constexpr int NSEG = KW / 16;  // 64-byte segments of a row's K slice
+  static_assert(KW % KS == 0 && K1 % 32 == 0, "k steps never straddle A1 / A2");
+  constexpr bool UV = S1 || (S2 && !YT);  // y tiles read A1 only; their LN2 residual uses 16-lane stats
+  floatx4* uv_s = reinterpret_cast<floatx4*>(smem);                        // [2][KT / 4]
+  char* a_s = smem + L::UV + (threadIdx.x >> 6) * L::AW;                   // this wave's fragments
+  float* red = reinterpret_cast<float*>(smem + L::UV + 4 * L::AW);        // [4][BM][BN + 1]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane >> 2;  // coalesced layout: row within a 16-row block
+  const int c = lane & 3;   //                   16-byte piece of a 64-byte segment
+  const int kbeg = wave * KW;
+  const int B = p.B;
+  const int ldw = YT ? K1 : K1 + kD;
+  const int wt0 = (YT ? c0 : c0 - p.NY) / 16;  // first 16-column tile of W
+
+  // ---- every load first
+  floatx4 u4{}, v4{};
+  const int kk4 = min(tid * 4, KT - 4);
+  if constexpr (UV) {
+    static_assert(KT / 4 <= 256, "one float4 of u and of v per thread");
+    const bool in1 = kk4 < K1;
+    const float* us = in1 ? (S1 ? p.a1_s + kk4 : p.a2_g) : (S2 ? p.a2_g + (kk4 - K1) : p.a2_g);
+    const float* vs = in1 ? (S1 ? p.a1_c + kk4 : p.a2_b) : (S2 ? p.a2_b + (kk4 - K1) : p.a2_b);
+    u4 = *reinterpret_cast<const floatx4*>(us);
+    v4 = *reinterpret_cast<const floatx4*>(vs);
+  }
+  int qrow[MF];
+#pragma unroll
+  for (int mf = 0; mf < MF; ++mf) qrow[mf] = min(r0 + mf * 16 + q, B - 1);  // rows >= B: discarded outputs
+  Part4 pa1[MF], pa2[MF];
+#pragma unroll
+  for (int mf = 0; mf < MF; ++mf) {
+    if constexpr (S1) pa1[mf] = load_part4(p.a1_stats + (size_t)qrow[mf] * 2 * kSlices, c);
+    if constexpr (S2 && !YT) pa2[mf] = load_part4(p.a2_stats + (size_t)qrow[mf] * 2 * kSlices, c);
+  }
+  floatx4 ra[MF][NSEG];
+#pragma unroll
+  for (int mf = 0; mf < MF; ++mf)
+#pragma unroll
+    for (int sg = 0; sg < NSEG; ++sg) {
+      const int k = kbeg + sg * 16 + c * 4;
+      const bool in1 = kbeg + sg * 16 < K1;  // wave-uniform
+      ra[mf][sg] = *reinterpret_cast<const floatx4*>(in1 ? p.A1 + (size_t)qrow[mf] * K1 + k
+                                                           : p.A2 + (size_t)qrow[mf] * kD + (k - K1));
+    }
+  floatx4 rw[NF][NKS][X3 ? 2 : 1];
+#pragma unroll
+  for (int nf = 0; nf < NF; ++nf)
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      const size_t fo = ((size_t)(wt0 + nf) * (ldw / KS) + kbeg / KS + s) * 64 + lane;
+      if constexpr (X3) {
+        rw[nf][s][0] = reinterpret_cast<const floatx4*>(YT ? p.Fy_hi : p.Fz_hi)[fo];
+        rw[nf][s][1] = reinterpret_cast<const floatx4*>(YT ? p.Fy_lo : p.Fz_lo)[fo];
+      } else {
+        rw[nf][s][0] = reinterpret_cast<const floatx4*>(YT ? p.Fy : p.Fz)[fo];
+      }
+    }
+  // epilogue operands (row = tid >> 4 of each 16-row block, column = tid & 15 of each
+  // 16-column block)
+  const int erow = tid >> 4;
+  const int ecol = tid & 15;
+  float rres[YT ? MF : 1][YT ? NF : 1], ebias[NF], eg[YT && S2 ? NF : 1], eb[YT && S2 ? NF : 1];
+  float2 est[YT && S2 ? MF : 1];
+#pragma unroll
+  for (int nf = 0; nf < NF; ++nf) {
+    const int col = (YT ? c0 : c0 - p.NY) + nf * 16 + ecol;
+    ebias[nf] = (YT ? p.by : p.bz)[col];
+    if constexpr (YT && S2) {
+      eg[nf] = p.a2_g[col];
+      eb[nf] = p.a2_b[col];
+    }
+  }
+  if constexpr (YT) {
+#pragma unroll
+    for (int mf = 0; mf < MF; ++mf) {
+      const int srow = min(r0 + mf * 16 + erow, B - 1);
+#pragma unroll
+      for (int nf = 0; nf < NF; ++nf) rres[mf][nf] = p.A2[(size_t)srow * kD + c0 + nf * 16 + ecol];
+      if constexpr (S2) est[mf] = reinterpret_cast<const float2*>(p.a2_stats + (size_t)srow * 2 * kSlices)[ecol];
+    }
+  }
+
+  // ---- A: transform, split, fragments to LDS
+  if constexpr (UV) {
+    if (tid * 4 < KT) {
+      uv_s[kk4 / 4] = u4;
+      uv_s[KT / 4 + kk4 / 4] = v4;
+    }
+    __syncthreads();
+  }
+  float m1[MF], rs1[MF], m2[MF], rs2[MF];
+#pragma unroll
+  for (int mf = 0; mf < MF; ++mf) {
+    m1[mf] = rs1[mf] = m2[mf] = rs2[mf] = 0.f;
+    if constexpr (S1) merge_part4_quad(pa1[mf], c, m1[mf], rs1[mf]);
+    if constexpr (S2 && !YT) merge_part4_quad(pa2[mf], c, m2[mf], rs2[mf]);
+  }
+#pragma unroll
+  for (int mf = 0; mf < MF; ++mf)
+#pragma unroll
+    for (int sg = 0; sg < NSEG; ++sg) {
+      floatx4 x = ra[mf][sg];
+      const int kl = kbeg + sg * 16 + c * 4;  // the tile's k of x[0]
+      const bool in1 = kbeg + sg * 16 < K1;
+      if ((S1 && in1) || (S2 && !YT && !in1)) {
+        const floatx4 u = uv_s[kl / 4];
+        const floatx4 v = uv_s[KT / 4 + kl / 4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (in1) {
+            if constexpr (S1) x[e] = fmaxf(fmaf(rs1[mf], fmaf(-m1[mf], u[e], x[e]), v[e]), 0.f);
+          } else {
+            if constexpr (S2 && !YT) x[e] = fmaf((x[e] - m2[mf]) * rs2[mf], u[e], v[e]);
+          }
+        }
+      }
+      if constexpr (X3) {
+        // step sg / 2; k within the step (sg % 2) 16 + 4 c = 8 g_t + 4 (c & 1)
+        const int lt = q + 16 * ((sg & 1) * 2 + (c >> 1));
+        uint32_t h0, l0, h1, l1;
+        split2_bf16(x[0], x[1], h0, l0);
+        split2_bf16(x[2], x[3], h1, l1);
+        char* f = a_s + ((sg / 2) * MF + mf) * 2048 + lt * 16 + (c & 1) * 8;
+        *reinterpret_cast<uint2*>(f) = make_uint2(h0, h1);
+        *reinterpret_cast<uint2*>(f + 1024) = make_uint2(l0, l1);
+      } else {
+        const int lt = q + 16 * c;  // chunk sg; k within it 4 c
+        *reinterpret_cast<floatx4*>(a_s + (sg * MF + mf) * 1024 + lt * 16) = x;
+      }
+    }
+  __syncthreads();  // fragments in LDS (each wave reads its own; lanes cross)
+
+  // ---- MFMAs
+  floatx4 acc[MF][NF];
+#pragma unroll
+  for (int mf = 0; mf < MF; ++mf)
+#pragma unroll
+    for (int nf = 0; nf < NF; ++nf) acc[mf][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NKS; ++s) {
+    if constexpr (X3) {
+      bf16x8 ah[MF], al[MF];
+#pragma unroll
+      for (int mf = 0; mf < MF; ++mf) {
+        const char* f = a_s + (s * MF + mf) * 2048 + lane * 16;
+        ah[mf] = *reinterpret_cast<const bf16x8*>(f);
+        al[mf] = *reinterpret_cast<const bf16x8*>(f + 1024);
+      }
+#pragma unroll
+      for (int mf = 0; mf < MF; ++mf)
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf) {
+          const bf16x8 bh = __builtin_bit_cast(bf16x8, rw[nf][s][0]);
+          const bf16x8 bl = __builtin_bit_cast(bf16x8, rw[nf][s][1]);
+          acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mf], bh, acc[mf][nf], 0, 0, 0);
+          acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mf], bl, acc[mf][nf], 0, 0, 0);
+          acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[mf], bh, acc[mf][nf], 0, 0, 0);
+        }
+    } else {
+      floatx4 a[MF];
+#pragma unroll
+      for (int mf = 0; mf < MF; ++mf) a[mf] = *reinterpret_cast<const floatx4*>(a_s + (s * MF + mf) * 1024 + lane * 16);
+#pragma unroll
+      for (int mf = 0; mf < MF; ++mf)
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mf][e], rw[nf][s][0][e], acc[mf][nf], 0, 0, 0);
+    }
+  }
+
+  // ---- combine the 4 waves' partial tiles in a fixed order
+  const int g = lane >> 4;
+  const int li = lane & 15;
+#pragma unroll
+  for (int mf = 0; mf < MF; ++mf)
+#pragma unroll
+    for (int nf = 0; nf < NF; ++nf)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[(wave * BM + mf * 16 + g * 4 + r) * (BN + 1) + nf * 16 + li] = acc[mf][nf][r];
+  __syncthreads();
+  if (dec_skip(p.st, p.t)) return;
+#pragma unroll
+  for (int mf = 0; mf < MF; ++mf) {
+    const int orow = r0 + mf * 16 + erow;
+    float mean = 0.f, rstd = 0.f;
+    if constexpr (YT && S2) row_stats_16lanes_v(est[mf].x, est[mf].y, ecol, mean, rstd);
+#pragma unroll
+    for (int nf = 0; nf < NF; ++nf) {
+      const int lr = mf * 16 + erow, lc = nf * 16 + ecol;
+      const float val = ((red[(0 * BM + lr) * (BN + 1) + lc] + red[(1 * BM + lr) * (BN + 1) + lc]) +
+                         red[(2 * BM + lr) * (BN + 1) + lc]) + red[(3 * BM + lr) * (BN + 1) + lc];
+      const int ocol = c0 + nf * 16 + ecol;
+      if constexpr (YT) {
+        float res = rres[mf][nf];
+        if constexpr (S2) res = fmaf((res - mean) * rstd, eg[nf], eb[nf]);
+        const float y = res + (val + ebias[nf]);
+        const float m16 = row_sum<16>(y) * (1.0f / 16);
+        const float qq = row_sum<16>((y - m16) * (y - m16));
+        if (orow < B) {
+          p.y[(size_t)orow * kD + ocol] = y;
+          if (ecol == 0) {
+            float* so = p.y_stats + ((size_t)orow * kSlices + ocol / 16) * 2;
+            so[0] = m16;
+            so[1] = qq;
+          }
+        }
+      } else if constexpr (LOGITS) {
+        const int zc = ocol - p.NY;
+        const float v = val + ebias[nf];
+        const bool cv = zc < p.n_valid;
+        if (orow < B && cv) p.z[(p.hist_stride ? (size_t)p.t * p.hist_stride : 0) + (size_t)orow * p.NZ + zc] = v;
+        if (p.part) {
+          // the 16-column tile's (max, first argmax, sum exp(l - max)) over the row's 16
+          // lanes (DPP quad_perm xor 1, xor 2, row_half_mirror, row_mirror)
+          float m = cv ? v : -INFINITY;
+          int ix = zc;
+          auto step = [&](float om, int oi) {
+            if (om > m || (om == m && oi < ix)) {
+              m = om;
+              ix = oi;
+            }
+          };
+          step(dpp<0xB1>(m), __builtin_amdgcn_mov_dpp(ix, 0xB1, 0xF, 0xF, false));
+          step(dpp<0x4E>(m), __builtin_amdgcn_mov_dpp(ix, 0x4E, 0xF, 0xF, false));
+          step(dpp<0x141>(m), __builtin_amdgcn_mov_dpp(ix, 0x141, 0xF, 0xF, false));
+          step(dpp<0x140>(m), __builtin_amdgcn_mov_dpp(ix, 0x140, 0xF, 0xF, false));
+          const float e = row_sum<16>(cv ? expf(v - m) : 0.f);
+          if (ecol == 0 && orow < B)
+            reinterpret_cast<floatx4*>(p.part)[(size_t)orow * (p.NZ / 16) + zc / 16] =
+                floatx4{m, __int_as_float(ix), e, 0.f};
+        }
+      } else {
+        const int zc = ocol - p.NY;
+        if (orow < B) p.z[(size_t)orow * p.NZ + zc] = val + ebias[nf];
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int K1, bool S1, bool S2, bool X3, bool LOGITS>
+__global__ void __launch_bounds__(256) foldwide_kernel(FoldGemmParams p) {
+  constexpr int BYTES = LOGITS ? TileLds<BM, BN, false, 0, X3>::BYTES
+                               : (TileLds<BM, BN, true, K1, X3>::BYTES > TileLds<BM, BN, false, K1, X3>::BYTES
+                                      ? TileLds<BM, BN, true, K1, X3>::BYTES
+                                      : TileLds<BM, BN, false, K1, X3>::BYTES);
+  __shared__ __attribute__((aligned(16))) char smem[BYTES];
+  const int ncol = (p.NY + p.NZ) / BN;
+  const int b = blockIdx.x;
+  const int c0 = (b % ncol) * BN;
+  const int r0 = (b / ncol) * BM;
+  if constexpr (LOGITS) {
+    wide_tile<BM, BN, false, 0, false, true, X3, true>(p, r0, c0, smem);
+  } else {
+    if (c0 < p.NY)
+      wide_tile<BM, BN, true, K1, S1, S2, X3, false>(p, r0, c0, smem);
+    else
+      wide_tile<BM, BN, false, K1, S1, S2, X3, false>(p, r0, c0, smem);
+  }
+}
+
+// Fragment-major copy of a row-major [N, K] fp32 weight (N % 16 == 0, K % 32 == 0):
+// X3 planes hi / lo [N/16][K/32][64 lanes][8] (bf16 split as split2_bf16), or fp32
+// [N/16][K/16][64 lanes][4]; lane L holds W[16 j + (L & 15)][k0 + (8 or 4) (L >> 4) + e].
+__global__ void frag_pack_kernel(const float* __restrict__ W, int N, int K, uint16_t* __restrict__ hi,
+                                 uint16_t* __restrict__ lo, float* __restrict__ f32) {
+  const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // one lane-chunk
+  const bool x3 = hi != nullptr;
+  const int ks = x3 ? 32 : 16, per = x3 ? 8 : 4;
+  const size_t nchunks = (size_t)N * K / per;
+  if (idx >= nchunks) return;
+  const int L = idx % 64;
+  const size_t t = idx / 64;
+  const int s = t % (K / ks);
+  const int j = t / (K / ks);
+  const float* src = W + (size_t)(16 * j + (L & 15)) * K + s * ks + per * (L >> 4);
+  if (x3) {
+    uint32_t h[4], l[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split2_bf16(src[2 * e], src[2 * e + 1], h[e], l[e]);
+    reinterpret_cast<uint4*>(hi)[idx] = make_uint4(h[0], h[1], h[2], h[3]);
+    reinterpret_cast<uint4*>(lo)[idx] = make_uint4(l[0], l[1], l[2], l[3]);
+  } else {
+    reinterpret_cast<floatx4*>(f32)[idx] = floatx4{src[0], src[1], src[2], src[3]};
+  }
+}
+
+template <int BM, int BN, bool X3, bool LOGITS>
+void launch_fw(const FoldGemmParams& p, hipStream_t s) {
+  const int ncol = (p.NY + p.NZ) / BN;
+  const dim3 grid(ncol * ((p.B + BM - 1) / BM));
+  if constexpr (LOGITS) {
+    foldwide_kernel<BM, BN, 0, false, true, X3, true><<<grid, 256, 0, s>>>(p);
+  } else {
+    const bool s1 = p.a1_stats != nullptr, s2 = p.a2_stats != nullptr;
+    if (p.K1 == 256 && !s1 && !s2) {
+      foldwide_kernel<BM, BN, 256, false, false, X3, false><<<grid, 256, 0, s>>>(p);
+    } else if (p.K1 == 256 && !s1 && s2) {
+      foldwide_kernel<BM, BN, 256, false, true, X3, false><<<grid, 256, 0, s>>>(p);
+    } else if (p.K1 == 512 && s1 && s2) {
+      foldwide_kernel<BM, BN, 512, true, true, X3, false><<<grid, 256, 0, s>>>(p);
+    } else {
+      throw std::runtime_error("foldwide: built for (K1 256, A2 plain or LayerNorm), (K1 512, both), logits");
+    }
+  }
+}
+
+}  // namespace
+
+// Wide fold GEMM (y tiles + z tiles) or, with p.K1 == 0 and the logits fields, fc_out.
+void launch_foldwide(const FoldGemmParams& p, hipStream_t s) {
+  const bool logits = p.K1 == 0;
+  const bool x3 = logits ? p.Fz_hi != nullptr : p.Fy_hi != nullptr;
+  if (logits) {
+    if (p.NY != 0 || !p.a2_stats || !p.a2_g || !p.a2_b || !p.A2 || !p.bz || !p.z || p.NZ % 32 != 0)
+      throw std::runtime_error("foldwide logits: A2 with LayerNorm, no y, NZ % 32 == 0");
+  } else {
+    if (p.NY != kD || p.NZ % 32 != 0 || (p.NZ && (!p.bz || !p.z)))
+      throw std::runtime_error("foldwide: NY == d and NZ a multiple of 32 with bz, z");
+    if (!p.A1 || !p.A2 || !p.by || !p.y || !p.y_stats) throw std::runtime_error("foldwide: null operand");
+  }
+  if ((p.a1_stats && (!p.a1_s || !p.a1_c)) || (p.a2_stats && (!p.a2_g || !p.a2_b)))
+    throw std::runtime_error("foldwide: statistics need their vectors");
+  const bool need_z = logits || p.NZ > 0;
+  const bool have = x3 ? (!need_z || (p.Fz_hi && p.Fz_lo)) && (logits || (p.Fy_hi && p.Fy_lo))
+                       : (!need_z || p.Fz) && (logits || p.Fy);
+  if (!have) throw std::runtime_error("foldwide: fragment-major weights (launch_frag_pack) missing");
+  if (p.B <= 0) return;
+  // fold GEMMs: 16-row tiles up to 64 rows (more workgroups for a short chain), 32 above
+  if (logits) {  // 16-row tiles at every R: fc_out's 159 column tiles x R / 16 fill the chip
+    if (x3) launch_fw<16, 32, true, true>(p, s); else launch_fw<16, 32, false, true>(p, s);
+  } else if (p.B <= 64) {
+    if (x3) launch_fw<16, 32, true, false>(p, s); else launch_fw<16, 32, false, false>(p, s);
+  } else {
+    if (x3) launch_fw<32, 32, true, false>(p, s); else launch_fw<32, 32, false, false>(p, s);
+  }
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_frag_pack(const float* W, int N, int K, uint16_t* hi, uint16_t* lo, float* f32, hipStream_t s) {
+  if (N % 16 != 0 || K % 32 != 0 || (!hi != !lo) || (!hi && !f32)) throw std::runtime_error("frag_pack: N % 16, K % 32");
+  const size_t chunks = (size_t)N * K / (hi ? 8 : 4);
+  frag_pack_kernel<<<(unsigned)((chunks + 255) / 256), 256, 0, s>>>(W, N, K, hi, lo, f32);
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace mocr

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -233,7 +234,8 @@ void check_config(const mocr_config& c) {
           c.precision == MOCR_PRECISION_BF16X3,
       "precision");
   req((c.variant & ~(MOCR_VARIANT_UNFUSED_ATTN | MOCR_VARIANT_UNFUSED_MLP | MOCR_VARIANT_DEC_UNFOLDED |
-                      MOCR_VARIANT_S4_FUSED_ATTN | MOCR_VARIANT_WINDOW_ROWS)) == 0,
+                      MOCR_VARIANT_S4_FUSED_ATTN | MOCR_VARIANT_WINDOW_ROWS | MOCR_VARIANT_DEC_NARROW |
+                      MOCR_VARIANT_LOGITS_F32)) == 0,
       "variant: unknown MOCR_VARIANT_* flag");
   req(c.sos_id >= 0 && c.sos_id < c.vocab && c.eos_id >= 0 && c.eos_id < c.vocab, "special ids");
 }
@@ -340,6 +342,15 @@ struct mocr_engine {
   uint16_t *fold_h = nullptr, *fold_l = nullptr;  // bf16x3: hi / lo planes of fold_buf
   float *qtab = nullptr, *qpos = nullptr, *dzqkv = nullptr;
   float* dpart = nullptr;  // greedy: logits tile partials [rows][Vpad/16] float4 for the argmax
+  // decwide.hip: fragment-major copies (launch_frag_pack) of every layer's fold GEMM weights
+  // (y_sa, z_q, y_ca, z_h, y_ff, z_qkv) and of fc_out; bf16x3 hi / lo planes or fp32
+  struct FragW {
+    uint16_t *hi = nullptr, *lo = nullptr;
+    float* f = nullptr;
+  };
+  std::vector<std::array<FragW, 6>> fragw;
+  FragW frag_logits;
+  std::vector<void*> frag_allocs;
 
   // timing
   bool timing = false;
@@ -366,6 +377,8 @@ struct mocr_engine {
                     HIDh, HIDl, MEMh, MEMl, dwh, dwl, kvwh, kvwl, bscore, bfin, bseq[0], bseq[1],
                     bslot[0], bslot[1], fold_buf, qtab, qpos, dzqkv, dpart};
     for (void* p : bufs)
+      if (p) (void)hipFree(p);
+    for (void* p : frag_allocs)
       if (p) (void)hipFree(p);
     for (float* p : relbias)
       if (p) (void)hipFree(p);
@@ -655,7 +668,7 @@ struct mocr_engine {
     lay.reset(new Layout(cfg));
 
     const size_t B = cfg.max_batch;
-    Vpad = (cfg.vocab + 15) / 16 * 16;
+    Vpad = (cfg.vocab + 31) / 32 * 32;  // whole 32-column logits tiles (decwide.hip)
     const size_t d = cfg.d_model, L = cfg.n_layers;
     if (cfg.arch == MOCR_ARCH_RES18TRANS) {
       init_res18();
@@ -749,6 +762,8 @@ struct mocr_engine {
       for (int i = 0; i < 2; ++i) {
         bseq[i] = dalloc<int32_t>(R * ld_ids);
         bslot[i] = dalloc<int32_t>(R * ld_ids);
+        MOCR_HIP_CHECK(hipMemset(bseq[i], 0, R * ld_ids * sizeof(int32_t)));
+        MOCR_HIP_CHECK(hipMemset(bslot[i], 0, R * ld_ids * sizeof(int32_t)));
       }
     }
     if (fold_greedy()) {
@@ -794,6 +809,7 @@ struct mocr_engine {
     st = dalloc<DecodeState>(1);
     MOCR_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&st_host), 2 * sizeof(DecodeState), hipHostMallocDefault));
     for (auto& e : chunk_ev) MOCR_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    MOCR_HIP_CHECK(hipDeviceSynchronize());  // null-stream memsets above vs the non-blocking stream
   }
 
   // [type][h][64 q][64 key] table of the bf16 attention kernel: bias[h][q][key] plus the
@@ -874,6 +890,7 @@ struct mocr_engine {
       MOCR_HIP_CHECK(hipStreamSynchronize(stream));
     }
     if (fold_greedy()) fold_decoder();
+    if (fold_wide()) pack_frags();
     MOCR_HIP_CHECK(hipDeviceSynchronize());
     weights_loaded = true;
     encoded = false;
@@ -919,6 +936,41 @@ struct mocr_engine {
     launch_fold_mm(W(lay->pos), d, nullptr, W(l0.sa_inw), 1, d, d, nullptr, nullptr, qpos, 3 * d, cfg.max_pos, 3 * d, s);
     if (fold_h) launch_split_bf16(fold_buf, fold_h, fold_l, fold_floats, s);
     MOCR_HIP_CHECK(hipStreamSynchronize(s));
+  }
+
+  // Fragment-major weights of the wide fold GEMMs and logits (decwide.hip), packed from the
+  // fp32 sources after fold_decoder: bf16x3 planes in bf16x3 engines, fp32 otherwise.
+  // The buffers are allocated by the first load and repacked in place by later ones: the
+  // captured decode graphs hold their addresses.
+  void pack_frag(FragW& f, const float* W, int N, int K, bool x3) {
+    const size_t n = (size_t)N * K;
+    if (x3 && !f.hi) {
+      f.hi = dalloc<uint16_t>(n);
+      f.lo = dalloc<uint16_t>(n);
+      frag_allocs.push_back(f.hi);
+      frag_allocs.push_back(f.lo);
+    } else if (!x3 && !f.f) {
+      f.f = dalloc<float>(n);
+      frag_allocs.push_back(f.f);
+    }
+    launch_frag_pack(W, N, K, f.hi, f.lo, f.f, stream);
+  }
+  void pack_frags() {
+    const int d = cfg.d_model, ff = cfg.d_ff, L = cfg.n_layers;
+    const bool x3 = fold_h != nullptr;
+    if (fragw.empty()) fragw.resize(L);
+    for (int l = 0; l < L; ++l) {
+      const DecLayerW& w = lay->layers[l];
+      const FoldW& f = foldw[l];
+      pack_frag(fragw[l][0], W(w.sa_ow), d, d, x3);
+      pack_frag(fragw[l][1], f.wzq, d, 2 * d, x3);
+      pack_frag(fragw[l][2], W(w.ca_ow), d, d, x3);
+      pack_frag(fragw[l][3], f.wzh, ff, 2 * d, x3);
+      pack_frag(fragw[l][4], W(w.l2w), d, ff, x3);
+      if (l + 1 < L) pack_frag(fragw[l][5], f.wzqkv, 3 * d, ff + d, x3);
+    }
+    pack_frag(frag_logits, fcw_pad, Vpad, d, logits_x3());
+    MOCR_HIP_CHECK(hipStreamSynchronize(stream));
   }
 
   void set_images(const float* src, int B, hipMemcpyKind kind) {
@@ -990,6 +1042,24 @@ struct mocr_engine {
   bool attn_fused() const { return !(cfg.variant & MOCR_VARIANT_UNFUSED_ATTN); }
   bool mlp_fused() const { return !(cfg.variant & MOCR_VARIANT_UNFUSED_MLP); }
   bool fold_greedy() const { return !(cfg.variant & MOCR_VARIANT_DEC_UNFOLDED); }
+  // wide-tile fold GEMMs and logits (decwide.hip) unless MOCR_VARIANT_DEC_NARROW
+  bool fold_wide() const { return fold_greedy() && !(cfg.variant & MOCR_VARIANT_DEC_NARROW); }
+  // the wide logits on bf16x3 MFMA (fc_out planes) in bf16x3 engines unless MOCR_VARIANT_LOGITS_F32
+  bool logits_x3() const {
+    return fold_wide() && cfg.precision == MOCR_PRECISION_BF16X3 && !(cfg.variant & MOCR_VARIANT_LOGITS_F32);
+  }
+  void fold_gemm(FoldGemmParams& g, hipStream_t s, int layer, int which) {
+    if (fold_wide()) {
+      g.NY = cfg.d_model;
+      const FragW& fy = fragw[layer][2 * which];
+      const FragW& fz = fragw[layer][2 * which + 1];
+      g.Fy_hi = fy.hi; g.Fy_lo = fy.lo; g.Fy = fy.f;
+      g.Fz_hi = fz.hi; g.Fz_lo = fz.lo; g.Fz = fz.f;
+      launch_foldwide(g, s);
+    } else {
+      launch_foldgemm(g, s);
+    }
+  }
   // stage 3 always (285 vs 301 us per block unfused at B=64, 384²); stage 4 only on request
   // (258 vs 211 us: a window's 64 padded rows re-read all of W_qkv, 1.8 GB from L2 per block,
   // and the padding costs 1.3x the GEMM's MFMA work)
@@ -1362,7 +1432,7 @@ struct mocr_engine {
       g.Wy = W(w.sa_ow); g.by = W(w.sa_ob); g.y = dy_sa; g.y_stats = ds_sa;
       g.Wz = f.wzq; g.bz = f.bzq; g.z = dq; g.NZ = d;
       fold_planes(g, w.sa_ow);
-      launch_foldgemm(g, s);
+      fold_gemm(g, s, l, 0);
       // y_ca = LN1(y_sa) + CA(LN1(y_sa), mem): attention, then out_proj + z_h = W_1' y_ca
       const float* memk = MEMKV + l * kv_layer;
       a = FoldAttnParams{};
@@ -1375,7 +1445,7 @@ struct mocr_engine {
       g.Wy = W(w.ca_ow); g.by = W(w.ca_ob); g.y = dy_ca; g.y_stats = ds_ca;
       g.Wz = f.wzh; g.bz = f.bzh; g.z = dh; g.NZ = cfg.d_ff;
       fold_planes(g, w.ca_ow);
-      launch_foldgemm(g, s);
+      fold_gemm(g, s, l, 1);
       // y_ff = LN2(y_ca) + W_2 relu(unfold(z_h)) + b_2, and the next layer's z_qkv
       g = FoldGemmParams{};
       g.B = B; g.t = t; g.st = stp;
@@ -1384,7 +1454,7 @@ struct mocr_engine {
       g.Wy = W(w.l2w); g.by = W(w.l2b); g.y = dy_ff; g.y_stats = ds_ff;
       if (l + 1 < L) { g.Wz = f.wzqkv; g.bz = f.bzqkv; g.z = dzqkv; g.NZ = 3 * d; }
       fold_planes(g, w.l2w);
-      launch_foldgemm(g, s);
+      fold_gemm(g, s, l, 2);
     }
   }
 
@@ -1392,6 +1462,16 @@ struct mocr_engine {
   void record_logits(int B, int t, const DecodeState* stp, float* out, size_t hist_stride, float* part = nullptr) {
     const int d = cfg.d_model, L = cfg.n_layers;
     const DecLayerW& last = lay->layers[L - 1];
+    if (part && fold_wide()) {  // the greedy step: fc_out on decwide.hip's tiles
+      FoldGemmParams g{};
+      g.B = B; g.t = t; g.st = stp; g.K1 = 0; g.NY = 0;
+      g.A2 = dy_ff; g.a2_stats = ds_ff; g.a2_g = W(last.n3w); g.a2_b = W(last.n3b);
+      g.Wz = fcw_pad; g.bz = fcb_pad; g.z = out; g.NZ = Vpad; g.n_valid = cfg.vocab; g.hist_stride = hist_stride;
+      g.part = part;
+      g.Fz_hi = frag_logits.hi; g.Fz_lo = frag_logits.lo; g.Fz = frag_logits.f;
+      launch_foldwide(g, stream);
+      return;
+    }
     RowGemmParams p{};
     p.B = B;
     p.st = stp;

@@ -71,6 +71,9 @@ struct mocr_group {
   ncclComm_t comm = nullptr;
   int world = 0, rank = 0, device = 0;
   hipStream_t stream = nullptr;
+  hipEvent_t ready = nullptr;  // the caller's stream state, waited on by the group stream
+  int32_t* shapes = nullptr;   // device [world][2]: every rank's (rows, width), checked before a gather
+  int32_t* shapes_host = nullptr;
 };
 
 extern "C" {
@@ -102,12 +105,19 @@ int mocr_group_create(const uint8_t* id, int world, int rank, int hip_device, mo
     g->device = hip_device;
     MOCR_HIP_CHECK(hipSetDevice(hip_device));
     MOCR_HIP_CHECK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+    MOCR_HIP_CHECK(hipEventCreateWithFlags(&g->ready, hipEventDisableTiming));
+    MOCR_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&g->shapes), (size_t)world * 2 * sizeof(int32_t)));
+    MOCR_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&g->shapes_host), (size_t)world * 2 * sizeof(int32_t),
+                                 hipHostMallocDefault));
     check(rccl().comm_init_rank(&g->comm, world, uid, rank), "ncclCommInitRank");
     *out = g;
     return 0;
   } catch (const std::exception& ex) {
     if (g) {
       if (g->stream) (void)hipStreamDestroy(g->stream);
+      if (g->ready) (void)hipEventDestroy(g->ready);
+      if (g->shapes) (void)hipFree(g->shapes);
+      if (g->shapes_host) (void)hipHostFree(g->shapes_host);
       delete g;
     }
     if (out) *out = nullptr;
@@ -120,15 +130,36 @@ int mocr_group_destroy(mocr_group* g) {
   (void)hipSetDevice(g->device);
   if (g->comm) (void)rccl().comm_destroy(g->comm);
   if (g->stream) (void)hipStreamDestroy(g->stream);
+  if (g->ready) (void)hipEventDestroy(g->ready);
+  if (g->shapes) (void)hipFree(g->shapes);
+  if (g->shapes_host) (void)hipHostFree(g->shapes_host);
   delete g;
   return 0;
 }
 
-int mocr_group_gather_ids(mocr_group* g, const int32_t* ids_dev, int rows, int width, int32_t* ids_all_dev) {
+int mocr_group_gather_ids(mocr_group* g, const int32_t* ids_dev, int rows, int width, int32_t* ids_all_dev,
+                          void* producer_stream) {
   try {
     if (!g || !ids_dev || !ids_all_dev) throw std::runtime_error("null argument");
     if (rows < 0 || width < 1) throw std::runtime_error("rows / width out of range");
     MOCR_HIP_CHECK(hipSetDevice(g->device));
+    // the ids (and the reuse of ids_all_dev) are ordered behind the producer's stream
+    MOCR_HIP_CHECK(hipEventRecord(g->ready, static_cast<hipStream_t>(producer_stream)));
+    MOCR_HIP_CHECK(hipStreamWaitEvent(g->stream, g->ready, 0));
+    // every rank must pass the same shape: all-gather the (rows, width) pairs first, so an
+    // uneven shard fails here on every rank instead of hanging or corrupting the gather
+    const int32_t mine[2] = {rows, width};
+    MOCR_HIP_CHECK(hipMemcpyAsync(g->shapes + 2 * g->rank, mine, sizeof(mine), hipMemcpyHostToDevice, g->stream));
+    check(rccl().all_gather(g->shapes + 2 * g->rank, g->shapes, 2, ncclInt32, g->comm, g->stream), "ncclAllGather");
+    MOCR_HIP_CHECK(hipMemcpyAsync(g->shapes_host, g->shapes, (size_t)g->world * 2 * sizeof(int32_t),
+                                  hipMemcpyDeviceToHost, g->stream));
+    MOCR_HIP_CHECK(hipStreamSynchronize(g->stream));
+    for (int r = 0; r < g->world; ++r)
+      if (g->shapes_host[2 * r] != rows || g->shapes_host[2 * r + 1] != width)
+        throw std::runtime_error("mocr_group_gather_ids: rank " + std::to_string(r) + " passes [" +
+                                 std::to_string(g->shapes_host[2 * r]) + ", " + std::to_string(g->shapes_host[2 * r + 1]) +
+                                 "], rank " + std::to_string(g->rank) + " [" + std::to_string(rows) + ", " +
+                                 std::to_string(width) + "]: shards must be equal (pad them to the same rows)");
     check(rccl().all_gather(ids_dev, ids_all_dev, (size_t)rows * width, ncclInt32, g->comm, g->stream),
           "ncclAllGather");
     MOCR_HIP_CHECK(hipStreamSynchronize(g->stream));

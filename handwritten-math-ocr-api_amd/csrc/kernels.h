@@ -200,11 +200,27 @@ struct FoldGemmParams {
   int NZ;
   int B, t;
   const DecodeState* st;
+  // launch_foldwide only: y columns (d, or 0 for the logits), and the logits form (K1 = 0:
+  // z = fc_out LN(A2) + b into slot t * hist_stride, n_valid real columns, per-16-column
+  // partials `part` [B][NZ / 16] for the greedy selection)
+  int NY;
+  int n_valid;
+  size_t hist_stride;
+  float* part;
+  // launch_foldwide: Wy / Wz fragment-major (launch_frag_pack): bf16x3 hi / lo planes, or fp32
+  const uint16_t *Fy_hi, *Fy_lo, *Fz_hi, *Fz_lo;
+  const float *Fy, *Fz;
   // bf16x3 (optional): bf16 hi / lo planes of Wy and Wz; A is split on load and each
   // product is hi·hi + hi·lo + lo·hi on v_mfma_f32_16x16x32_bf16 (fp32 MFMA otherwise)
   const uint16_t *Wy_hi, *Wy_lo, *Wz_hi, *Wz_lo;
 };
 void launch_foldgemm(const FoldGemmParams& p, hipStream_t s);
+// The same fold GEMM on BM x BN tiles with the K range split over 4 waves (decwide.hip),
+// for decode chains of 64-256+ rows; with K1 = 0 the fc_out logits (+ partials).
+void launch_foldwide(const FoldGemmParams& p, hipStream_t s);
+// Fragment-major copy of a row-major [N, K] fp32 weight for launch_foldwide: bf16x3 hi / lo
+// planes (hi, lo non-null) or fp32 (f32).  N % 16 == 0, K % 32 == 0.
+void launch_frag_pack(const float* W, int N, int K, uint16_t* hi, uint16_t* lo, float* f32, hipStream_t s);
 
 // Attention of the newest position with folded inputs, one workgroup per (row, head):
 // q = rstd (z_q - mu s) + c from z [B, z_ld] and z_stats (plain z when z_stats is null).

@@ -23,9 +23,10 @@ LIB_PATH = os.path.join(_HERE, "lib", "libmathocr.so")
 PRECISION = {"fp32": 0, "bf16": 1, "bf16x3": 2}
 STOP = {"batch": 0, "none": 1}
 ARCH = {"swin": 0, "res18trans": 1}
-ABI_VERSION = 4
+ABI_VERSION = 5
 # kernel-path variants (include/mathocr.h MOCR_VARIANT_*): 0 = production
-VARIANT = {"unfused_attn": 1, "unfused_mlp": 2, "dec_unfolded": 4, "s4_fused_attn": 8, "window_rows": 16}
+VARIANT = {"unfused_attn": 1, "unfused_mlp": 2, "dec_unfolded": 4, "s4_fused_attn": 8, "window_rows": 16, "dec_narrow": 32,
+           "logits_f32": 64}
 
 
 class MocrConfig(ctypes.Structure):
@@ -78,7 +79,7 @@ def load_library(path: str = LIB_PATH):
         "mocr_group_create": (I, [ctypes.c_char_p, I, I, I, ctypes.POINTER(P)]),
         "mocr_group_destroy": (I, [P]),
         "mocr_group_last_error": (ctypes.c_char_p, []),
-        "mocr_group_gather_ids": (I, [P, P, I, I, P]),
+        "mocr_group_gather_ids": (I, [P, P, I, I, P, P]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)

@@ -74,8 +74,11 @@ class RcclGroup:
             out = torch.empty((self.world * rows, width), dtype=torch.int32, device=ids_local.device)
         if tuple(out.shape) != (self.world * rows, width) or not out.is_contiguous():
             raise ValueError("out must be a contiguous [world*rows, width] int32 tensor")
+        # the group stream waits for torch's current stream (the producer of ids_local, e.g.
+        # the .contiguous() copy above, and the last user of out's memory)
+        producer = torch.cuda.current_stream(ids_local.device).cuda_stream
         rc = self.lib.mocr_group_gather_ids(self._h, ctypes.c_void_p(ids_local.data_ptr()), rows, width,
-                                            ctypes.c_void_p(out.data_ptr()))
+                                            ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(producer))
         if rc != 0:
             raise MocrError(f"mocr_group_gather_ids failed ({rc}): {self.lib.mocr_group_last_error().decode()}")
         return out

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MOCR_ABI_VERSION 4
+#define MOCR_ABI_VERSION 5
 
 /* Arithmetic of the engine. */
 enum {
@@ -74,9 +74,13 @@ enum {
   MOCR_VARIANT_S4_FUSED_ATTN = 8, /* Swin stage 4 (C = 768): norm1 + qkv + W-MSA in one kernel (two  */
                                   /* 384-channel LDS halves) -- measured slower than the unfused     */
                                   /* sequence at 384x384, so off in production                       */
-  MOCR_VARIANT_WINDOW_ROWS = 16   /* unfused Swin attention (stage 4, or with UNFUSED_ATTN) over the */
+  MOCR_VARIANT_WINDOW_ROWS = 16,  /* unfused Swin attention (stage 4, or with UNFUSED_ATTN) over the */
                                   /* partitioned window rows, padded tokens included, instead of the */
                                   /* image's tokens in pixel order                                   */
+  MOCR_VARIANT_DEC_NARROW = 32,   /* folded greedy step on decfold.hip's 16x16-tile fold GEMMs and    */
+                                  /* decoder.hip's logits kernel instead of decwide.hip's wide tiles */
+  MOCR_VARIANT_LOGITS_F32 = 64    /* bf16x3 engines: the greedy step's fc_out on fp32-input MFMA     */
+                                  /* instead of bf16x3 (fc_out hi / lo planes)                        */
 };
 
 /* Greedy stopping rule (src/inference.py:23-25). */
@@ -213,11 +217,14 @@ int mocr_group_destroy(mocr_group* g);
 const char* mocr_group_last_error(void);
 
 /* Collective: every rank passes its shard's ids [rows, width] int32 (device memory, e.g.
- * the ids mocr_decode_device wrote; equal rows on every rank); ids_all_dev [world*rows,
- * width] receives all shards in rank order.  Runs on the group's HIP stream and returns
- * when the result is complete; the caller orders ids_dev's producer before the call
- * (mocr_decode_device returns after its copy has completed). */
-int mocr_group_gather_ids(mocr_group* g, const int32_t* ids_dev, int rows, int width, int32_t* ids_all_dev);
+ * the ids mocr_decode_device wrote); ids_all_dev [world*rows, width] receives all shards
+ * in rank order.  The group's HIP stream first waits for everything queued so far on
+ * producer_stream (the hipStream_t that wrote ids_dev or last used ids_all_dev, e.g.
+ * torch's current stream; NULL = the null stream), then all-gathers every rank's
+ * (rows, width) and fails on every rank, before the data gather, unless all are equal.
+ * Returns when the result is complete. */
+int mocr_group_gather_ids(mocr_group* g, const int32_t* ids_dev, int rows, int width, int32_t* ids_all_dev,
+                          void* producer_stream);
 
 #ifdef __cplusplus
 }

@@ -118,13 +118,15 @@ def test_teacher_forced_logits_384(pkg, g384):
     np.testing.assert_array_equal(res.ids[:, 1:], g["ids"][:, 1:])
 
 
+@pytest.mark.parametrize("variant", [(), ("logits_f32",)])
 @pytest.mark.parametrize("name", ["g384_b2_pert", "g96x320_b4_eos"])
-def test_teacher_forced_logits_bf16x3(pkg, golden, name):
-    """The bench precision (bf16x3 encoder GEMMs, attention and fold GEMMs of the decode
-    step): teacher-forced logits within the north star's 1e-3, ids token-exact."""
+def test_teacher_forced_logits_bf16x3(pkg, golden, name, variant):
+    """The bench precision (bf16x3 encoder GEMMs, attention, fold GEMMs and logits of the
+    decode step; MOCR_VARIANT_LOGITS_F32: fp32 logits): teacher-forced logits within the
+    north star's 1e-3, ids token-exact."""
     g = golden(name)
     m = g["meta"]
-    eng, _ = make_engine(pkg, m, precision="bf16x3")
+    eng, _ = make_engine(pkg, m, precision="bf16x3", variant=variant)
     eng.encode(pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m["img_kind"]))
     S = g["ids"].shape[1] - 1
     res = eng.decode(max_steps=S, stop="none", forced=g["ids"], want_logits=True)
@@ -138,12 +140,15 @@ def test_teacher_forced_logits_bf16x3(pkg, golden, name):
     assert np.array_equal(res.ids[:, 1:][ok], g["ids"][:, 1:][ok])
 
 
-def test_unfolded_decode_variant_matches_golden(pkg, golden):
-    """MOCR_VARIANT_DEC_UNFOLDED: the 8-kernel greedy step (LayerNorms applied by their
-    consumers) gives the fixture's ids and teacher-forced logits, as the folded step does."""
+@pytest.mark.parametrize("variant", [("dec_unfolded",), ("dec_narrow",)])
+def test_decode_variant_matches_golden(pkg, golden, variant):
+    """MOCR_VARIANT_DEC_UNFOLDED (the 8-kernel greedy step, LayerNorms applied by their
+    consumers) and MOCR_VARIANT_DEC_NARROW (the folded step on decfold.hip's 16x16-tile
+    GEMMs and decoder.hip's logits kernel instead of decwide.hip's wide tiles) give the
+    fixture's ids and teacher-forced logits, as the production step does."""
     g = golden("g96x320_b4_eos")
     m = g["meta"]
-    eng, _ = make_engine(pkg, m, variant=("dec_unfolded",))
+    eng, _ = make_engine(pkg, m, variant=variant)
     eng.encode(pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m["img_kind"]))
     res = eng.decode(max_steps=m["steps"], stop="batch")
     np.testing.assert_array_equal(res.ids, g["ids"])
@@ -221,6 +226,34 @@ def test_batch_invariance_384(pkg, g384):
     res = eng.decode(max_steps=g["meta"]["steps"], stop="none")
     np.testing.assert_array_equal(res.ids[0], g["ids"][1])
     eng.close()
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+def test_wide_chain_rows_bitwise(pkg, g384, precision):
+    """A 160-row decode chain (decwide.hip: 32-row fold-GEMM tiles, 64-row logits tiles,
+    a partial last tile) gives rows 0-1 bitwise the logits and ids of the 2-row chain
+    (16-row tiles): every output element sums the same k in the same order whatever the
+    tile height, so rows do not depend on the chain they decode in.  Rows 0-1 are the
+    B=2 fixture's images; their ids match the fixture."""
+    g, _, w, imgs = g384
+    S = 24
+    others = pkg.synth.make_images(158, 384, 384, seed0=5000)
+    big = np.concatenate([imgs, others], 0)
+    out, mem = {}, {}
+    for rows, x in ((160, big), (2, imgs)):
+        eng = pkg.Engine(img_hw=(384, 384), max_batch=rows, precision=precision)
+        eng.load_weights(w)
+        eng.encode(x)
+        mem[rows] = eng.memory()[:2]
+        out[rows] = eng.decode(max_steps=S, stop="none", want_logits=True)
+        eng.close()
+    np.testing.assert_array_equal(out[160].ids[:2], out[2].ids)
+    np.testing.assert_array_equal(out[2].ids, g["ids"][:, :S + 1])
+    if np.array_equal(mem[160], mem[2]):  # the encoder's GEMM dispatch kept the same k order
+        np.testing.assert_array_equal(out[160].logits[:2], out[2].logits)
+    else:
+        print("encoder memory differs between B=160 and B=2 (GEMM dispatch by M): logits compared within 1e-5")
+        np.testing.assert_allclose(out[160].logits[:2], out[2].logits, rtol=0, atol=1e-5)
 
 
 @pytest.mark.parametrize("precision,tol", [("bf16x3", 1e-4), ("bf16", 3e-2)])
