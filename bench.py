@@ -8,9 +8,16 @@
 A step = encode + 128-step greedy decode of one 64-image batch (images resident in HBM),
 then, with N > 1 ranks, an RCCL all-gather of the decoded token streams inside
 libmathocr.so (``mocr_group_gather_ids``; image-parallel shards, no other collective;
-torch.distributed over gloo carries only the group id, barriers and the timing max).  Each GPU pipelines its steps through R engine replicas
-(``pipeline.ReplicaPool``), so one batch's latency-bound decode overlaps the next
-batch's encoder; every step still runs the whole path on its own 64 images.  Rank 0
+torch.distributed over gloo carries only the group id, barriers and the timing max).
+
+Each engine call takes G = --chain-batches batches of 64 (default 4): one encode of the
+G*64 images and ONE decode chain of G*64 rows.  A greedy step is a chain of 41 dependent
+kernels whose launch and memory latencies do not grow with the rows, so G batches in one
+chain amortise them G ways (profiles/r03/decode_chain_probe_*.log); rows are
+independent (stop="none" here; tests/test_gpu_parity.py::test_wide_chain_rows_bitwise
+holds a row's logits bitwise equal between a 2-row and a 160-row chain).  Each GPU
+pipelines calls through R engine replicas (``pipeline.ReplicaPool``, one host thread and
+one HIP stream each), so one call's decode overlaps the next call's encoder.  Rank 0
 prints one JSON line; ``value`` = all images all ranks processed / max-over-ranks time.
 """
 from __future__ import annotations
@@ -47,12 +54,16 @@ def parse():
     ap.add_argument("--image", type=int, nargs=2, default=[384, 384])
     ap.add_argument("--tokens", type=int, default=128)
     ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3", "bf16"])
-    ap.add_argument("--replicas", type=int, default=4,
-                    help="engine replicas pipelining batches per GPU (throughput plateaus at 4-6: tools/pipeline_probe.py)")
+    ap.add_argument("--replicas", type=int, default=None,
+                    help="engine replicas pipelining calls per GPU (default: 2 with 4-batch chains, 4 with 1)")
+    ap.add_argument("--chain-batches", dest="chain", type=int, default=None,
+                    help="64-image batches per engine call / decode chain (default 4; 1 for res18trans, whose "
+                         "encoder attends across its batch, and for beam search)")
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
-    ap.add_argument("--cpu-sample", type=int, default=16,
-                    help="images per CPU-baseline throughput run (BASELINE.md §3; bounded to ~10-30 s in total)")
+    ap.add_argument("--cpu-sample", type=int, default=64,
+                    help="images per CPU-baseline throughput run (BASELINE.md §3: B = 64, median of 3)")
+    ap.add_argument("--cpu-runs", type=int, default=3)
     ap.add_argument("--no-isolated", dest="isolated", action="store_false", default=True,
                     help="skip the single-replica latency / roofline pass")
     ap.add_argument("--arch", default="swin", choices=["swin", "res18trans"],
@@ -62,6 +73,12 @@ def parse():
     a = ap.parse_args()
     if a.beam and a.arch != "swin":
         ap.error("--beam is measured on the Swin path")
+    if a.chain is None:
+        a.chain = 1 if (a.arch != "swin" or a.beam) else 4
+    if a.chain > 1 and (a.arch != "swin" or a.beam):
+        ap.error("--chain-batches > 1 is for the Swin greedy path (the ResNet18-trans encoder attends across its batch)")
+    if a.replicas is None:
+        a.replicas = 2 if a.chain > 1 else 4
     return a
 
 
@@ -96,8 +113,8 @@ def cpu_baseline(args, pkg):
         model_ref.greedy_decode(model, images=imgs[:batch], max_steps=args.tokens, stop="none")
         return time.perf_counter() - t0
 
-    lat = statistics.median(timed(1) for _ in range(3))
-    thr = statistics.median(timed(n) for _ in range(3))
+    lat = statistics.median(timed(1) for _ in range(args.cpu_runs))
+    thr = statistics.median(timed(n) for _ in range(args.cpu_runs))
     cpu = platform.processor() or platform.machine()
     try:
         cpu = next(ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name"))
@@ -105,7 +122,7 @@ def cpu_baseline(args, pkg):
         pass
     return {"value": n / thr, "unit": "images/sec", "cores": threads, "kind": "port",
             "b1_latency_ms": lat * 1e3, "cpu": cpu,
-            "sample": f"median of 3 runs of {n} images (and of 1 image for b1_latency_ms), {args.image[0]}x"
+            "sample": f"median of {args.cpu_runs} runs of {n} images (and of 1 image for b1_latency_ms), {args.image[0]}x"
                       f"{args.image[1]}, {args.tokens} greedy steps, full-prefix re-decode as src/inference.py, "
                       f"fp32 torch CPU, {threads} threads; {n}-image run {thr:.1f} s"}
 
@@ -121,13 +138,19 @@ def pmc_traffic(precision, cls):
         return None
 
 
+# per 384² image 26.39 GFLOP of encoder work at the dense bf16 MFMA peak
+# plus 245 MB of bf16 decode traffic at 8 TB/s
+E2E_ROOFLINE_IMG_S = 1.0 / (26.39e9 / 2.5e15 + 245e6 / 8e12)
+
+
 def roofline(stats, dtype, precision, attention=False):
     """Dominant encoder GEMM class (attention=False) or window-attention class
     (attention=True: the fused norm1 + qkv + W-MSA kernels, s3.attn at 384²) by
     event-timed GPU time: algorithmic FLOP per launch / average launch duration, against
     the dense bf16 MFMA peak (fp32 MFMA in fp32 mode).  bf16x3 issues three bf16 MFMAs per
     product (hi*hi + hi*lo + lo*hi), so the MFMA issue rate is 3x the algorithmic rate:
-    reported beside it as mfma_issue_frac."""
+    reported beside it as mfma_issue_frac.  peak_basis says which peak frac divides by
+    (round 1 divided bf16x3 by 2500/3; rounds 2-3 by 2500)."""
     gemms = {k: v for k, v in stats.items()
              if v["flops"] > 0 and ("attn" in k) == attention and not k.endswith("stem") and k != "r.enc"
              and not k.startswith("decode")}
@@ -141,6 +164,7 @@ def roofline(stats, dtype, precision, attention=False):
     kind = "attention" if attention else f"gemm_{'f32' if dtype == 'f32' else 'bf16'}"
     out = {"kernel": f"{kind}[{dtype}] {name}", "bound": "mfma",
            "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+           "peak_basis": "dense fp32 MFMA" if dtype == "f32" else "dense bf16 MFMA (2.5 PF)",
            "traffic": pmc_traffic(precision, name),
            "avg_launch_ms": avg_ms, "flops_per_launch": flops,
            "algorithmic_bytes_per_launch": d["bytes"] / d["launches"]}
@@ -149,20 +173,33 @@ def roofline(stats, dtype, precision, attention=False):
     return out
 
 
-def roofline_decode(stats, precision):
-    """The greedy decode step (41 graph-captured dependent kernels) against HBM: the
-    algorithmic bytes of a step (engine.hip decode_step_bytes: weights, cross-attention
-    K/V, self-attention K/V, logits; fp32 as built) / the HIP-event step time."""
+def survey_decode_step_bytes(rows, t, L=8, d=256, ff=512, V=5075, M=144):
+    """SURVEY.md §8(d)'s algorithmic bytes of one greedy step over `rows` rows, bf16: every
+    decoder weight and fc_out once, the cross-attention K/V of all layers, the
+    self-attention K/V of positions 0..t read and t written."""
+    weights = L * (6 * d * d + 2 * d * ff) + V * d
+    return 2.0 * (weights + rows * M * 2 * d * L + rows * (t + 2) * 2 * d * L)
+
+
+def roofline_decode(stats, precision, rows, steps):
+    """The greedy decode step (41 graph-captured dependent kernels) against HBM: SURVEY
+    §8(d)'s algorithmic bytes of a step (bf16 K/V and weights) / the HIP-event step time,
+    with the engine's fp32-as-built bytes (engine.hip decode_step_bytes) beside them."""
     d = stats.get("decode.greedy")
     if not d or not d["launches"]:
         return None
     step_ms = d["total_ms"] / d["launches"]
-    byts = d["bytes"] / d["launches"]
-    achieved = byts / (step_ms * 1e-3) / 1e9
-    return {"kernel": "greedy decode step (8 layers x 5 folded kernels + logits; the selection runs in the next step's first kernel)", "bound": "hbm",
+    built = d["bytes"] / d["launches"]
+    survey = sum(survey_decode_step_bytes(rows, t) for t in range(steps)) / steps
+    achieved = survey / (step_ms * 1e-3) / 1e9
+    return {"kernel": f"greedy decode step over {rows} rows (8 layers x 5 folded kernels + logits; the selection "
+                      f"runs in the next step's first kernel)", "bound": "hbm",
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "traffic": pmc_traffic(precision, "decode.step"), "avg_step_ms": step_ms,
-            "algorithmic_bytes_per_step": byts, "tflops": d["flops"] / d["launches"] / (step_ms * 1e-3) / 1e12}
+            "traffic": pmc_traffic(precision, "decode.step"), "avg_step_ms": step_ms, "rows": rows,
+            "algorithmic_bytes_per_step": survey, "bytes_basis": "SURVEY.md §8(d): bf16 weights and K/V",
+            "as_built_bytes_per_step": built, "as_built_achieved": built / (step_ms * 1e-3) / 1e9,
+            "as_built_frac": built / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "tflops": d["flops"] / d["launches"] / (step_ms * 1e-3) / 1e12}
 
 
 def main():
@@ -188,27 +225,30 @@ def main():
             grp = pkg.parallel.RcclGroup(world, rank, local)  # RCCL inside libmathocr.so
             gather = "rccl (mocr_group_gather_ids)"
     H, W = args.image
-    B, S, R = args.batch, args.tokens, args.replicas
+    B, S, R, G = args.batch, args.tokens, args.replicas, args.chain
+    BG = B * G  # images per engine call (one encode, one decode chain of BG rows)
     dtype = DTYPE[args.precision]
+    calls = -(-args.steps // G)  # timed engine calls; the line reports calls * G batches
+    wcalls = -(-args.warmup // G)
 
     # 256 beam-search tokens need a positional table of >= 257 rows (the reference's has 150,
     # src/model_swin.py:54): synthetic weights with 260 rows for that config
     max_pos = max(pkg.synth.MAX_POS, S + 4) if args.beam else pkg.synth.MAX_POS
-    ekw = dict(img_hw=(H, W), max_batch=B, precision=args.precision, device=local, arch=args.arch,
+    ekw = dict(img_hw=(H, W), max_batch=BG, precision=args.precision, device=local, arch=args.arch,
                max_beam=args.beam, max_pos=max_pos)
     pool = pkg.pipeline.ReplicaPool(R, **ekw)
     weights = pkg.synth.make_weights(1234, "init", arch=args.arch, max_pos=max_pos)
     pool.load_weights(weights)
-    # each replica holds its own batch of this rank's shard, resident in HBM
+    # each replica holds its own G batches of this rank's shard, resident in HBM
     for i, e in enumerate(pool.engines):
-        seed0 = 1000 + (rank * R + i) * B
-        e.set_images(torch.from_numpy(pkg.synth.make_images(B, H, W, seed0=seed0)).to(dev))
+        seed0 = 1000 + (rank * R + i) * BG
+        e.set_images(torch.from_numpy(pkg.synth.make_images(BG, H, W, seed0=seed0)).to(dev))
         if args.arch == "res18trans":
             e.set_encoder_pos(pkg.synth.make_pos_table(5, e.memory_tokens))
 
     def step(eng, _k):
         t0 = time.perf_counter()
-        ids = torch.empty((B, S + 1), dtype=torch.int32, device=dev)
+        ids = torch.empty((BG, S + 1), dtype=torch.int32, device=dev)
         eng.encode()
         if args.beam:
             r = eng.beam_search(beam=args.beam, max_steps=S, stop="none")
@@ -221,18 +261,18 @@ def main():
         lat = []
         for ids, dt in pool.imap(step, range(n)):
             if grp:
-                grp.gather_ids(ids)  # RCCL all-gather of the token streams, in step order
+                grp.gather_ids(ids)  # RCCL all-gather of the token streams, in call order
             elif world > 1:
                 pkg.parallel.gather_ids_host(ids.cpu(), world)
             lat.append(dt)
         return lat
 
-    run(args.warmup)
+    run(wcalls)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    lat = run(args.steps)
+    lat = run(calls)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -244,7 +284,7 @@ def main():
 
     iso = None
     if rank == 0 and args.isolated:
-        # one replica alone: unloaded batch latency + HIP-event kernel timing for the roofline
+        # one replica alone: unloaded call latency + HIP-event kernel timing for the roofline
         e = pool.engines[0]
         e.set_timing(True)
         ts = []
@@ -268,7 +308,7 @@ def main():
                 e1.decode(max_steps=S, stop="none")
             t1s.append(time.perf_counter() - t1)
         e1.close()
-        iso = {"batch_latency_ms": statistics.median(ts) * 1e3, "b1_latency_ms": statistics.median(t1s) * 1e3,
+        iso = {"call_latency_ms": statistics.median(ts) * 1e3, "b1_latency_ms": statistics.median(t1s) * 1e3,
                "stats": stats}
 
     if rank != 0:
@@ -279,14 +319,16 @@ def main():
             dist.destroy_process_group()
         return
 
+    steps = calls * G
+    value = world * B * steps / elapsed
     out = {
         "metric": METRIC,
-        "value": world * B * args.steps / elapsed,
+        "value": value,
         "unit": "images/sec",
         "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "steps": steps,
+        "warmup": wcalls * G,
+        "ms_per_step": elapsed / steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -301,21 +343,41 @@ def main():
                    "global_batch": world * B,
                    "per_gpu_batch": B, "image": [H, W], "max_tokens": S, "vocab": pkg.synth.VOCAB,
                    "decoder_layers": pkg.synth.N_LAYERS, "parallelism": f"image-parallel x{world}", "gather": gather,
-                   "replicas_per_gpu": R, "precision": args.precision},
+                   "replicas_per_gpu": R, "batches_per_chain": G, "precision": args.precision},
+        "e2e_roofline": {"value": value / world, "unit": "images/sec per GPU", "peak": E2E_ROOFLINE_IMG_S,
+                         "frac": value / world / E2E_ROOFLINE_IMG_S,
+                         "basis": "BASELINE.md §4: 26.39 GFLOP/img at 2.5 PF + 245 MB/img bf16 decode traffic at 8 TB/s"},
+        # latency of a 64-image batch under the bench's load: it completes with its call
+        "p50_batch_latency_loaded_ms": statistics.median(lat) * 1e3,
         "p50_image_latency_ms": statistics.median(lat) * 1e3,
+        "latency_note": (f"p50_image_latency_ms is the loaded latency of an image's call ({G} batch(es) of {B} "
+                         f"through encode + decode, {R} replicas pipelining); p50_image_latency_b1_ms is one image "
+                         f"alone (B=1)"),
     }
     if iso:
-        out["p50_image_latency_unloaded_ms"] = iso["batch_latency_ms"]
+        out["p50_batch_latency_unloaded_ms"] = iso["call_latency_ms"]
         out["p50_image_latency_b1_ms"] = iso["b1_latency_ms"]
-        out["roofline"] = roofline(iso["stats"], dtype, args.precision)
+        rd = roofline_decode(iso["stats"], args.precision, BG, S)
+        rg = roofline(iso["stats"], dtype, args.precision)
         ra = roofline(iso["stats"], dtype, args.precision, attention=True)
+        # `roofline` is the dominant kernel class by GPU time (HIP events, one call alone):
+        # the decode step when its share is the largest, else the dominant encoder GEMM
+        dec_ms = iso["stats"].get("decode.greedy", {}).get("total_ms", 0.0)
+        gemm_cls = max(((k, v) for k, v in iso["stats"].items() if not k.startswith(("decode", "host"))),
+                       key=lambda kv: kv[1]["total_ms"], default=(None, {"total_ms": 0.0}))
+        if rd and dec_ms >= gemm_cls[1]["total_ms"]:
+            out["roofline"] = rd
+            out["roofline_gemm"] = rg
+        else:
+            out["roofline"] = rg
+            if rd:
+                out["roofline_decode"] = rd
         if ra:
             out["roofline_attention"] = ra
-        rd = roofline_decode(iso["stats"], args.precision)
-        if rd:
-            out["roofline_decode"] = rd
-        out["encoder_ms_per_batch_events"] = sum(v["total_ms"] for k, v in iso["stats"].items()
-                                                 if not k.startswith(("decode", "host"))) / 3
+        enc_ms = sum(v["total_ms"] for k, v in iso["stats"].items() if not k.startswith(("decode", "host"))) / 3
+        out["gpu_time_share"] = {"decode": dec_ms / 3 / (dec_ms / 3 + enc_ms) if dec_ms else 0.0,
+                                 "encoder_ms_per_call": enc_ms, "decode_ms_per_call": dec_ms / 3}
+        out["encoder_ms_per_batch_events"] = enc_ms / G
         out["kernel_classes"] = {k: {"launches": v["launches"], "avg_ms": v["total_ms"] / v["launches"],
                                      "tflops": v["flops"] / v["total_ms"] * 1e-9 if v["total_ms"] else None}
                                  for k, v in sorted(iso["stats"].items())}

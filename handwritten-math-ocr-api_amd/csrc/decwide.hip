@@ -106,44 +106,47 @@ __device__ __forceinline__ void row_stats_16lanes(const float* __restrict__ part
   rstd = rstd_of(q);
 }
 
-// LDS of one tile: the k-vectors (u, v), each wave's transformed A fragments, the 4-wave
-// reduction.  X3: per (k step, row fragment) a hi and a lo 1-KB fragment; fp32: one.
-template <int BM, int BN, bool YT, int K1, bool X3>
+// LDS of one tile: the k-vectors (u, v), each wave's A fragments of one k step (reused
+// step after step: a wave's LDS accesses execute in order), the 4-wave reduction.
+template <int BM, int BN, bool YT, int K1, bool X3, int NW>
 struct TileLds {
   static constexpr int KT = YT ? K1 : K1 + kD;
-  static constexpr int KW = KT / 4;
   static constexpr int UV = 2 * KT * 4;
-  static constexpr int AW = (BM / 16) * (KW / (X3 ? 32 : 16)) * (X3 ? 2 : 1) * 1024;  // per wave
-  static constexpr int RED = 4 * BM * (BN + 1) * 4;
-  static constexpr int BYTES = UV + 4 * AW + RED;
+  static constexpr int AW = (BM / 16) * (X3 ? 2 : 1) * 1024;  // per wave: one step's fragments
+  static constexpr int RED = NW * BM * (BN + 1) * 4;
+  static constexpr int BYTES = UV + NW * AW + RED;
 };
 
 // One BM x BN tile.  KT = the tile's K (K1 for y tiles, K1 + d for z tiles); each of the
-// 4 waves takes KT / 4 consecutive k.
+// 4 waves takes KT / 4 consecutive k in steps of KS (32: bf16x3 16x16x32; 16: fp32 16x16x4
+// in four MFMAs).
+//  - Every load is issued up front, step by step (the step-s A pieces and W fragments
+//    together), so each step waits only for its own data.
 //  - A is loaded coalesced (lane = row (lane >> 2) x 16 bytes (lane & 3) of a 64-byte row
-//    segment, so every quad of lanes reads one segment), transformed once (FFN unfold +
-//    ReLU, LayerNorm), split into bf16 hi / lo (X3) and written to the wave's LDS region in
-//    MFMA fragment order; the k loop reads each fragment with one ds_read_b128.
+//    segment: every quad of lanes reads one segment), transformed once (FFN unfold + ReLU,
+//    LayerNorm), split into bf16 hi / lo (X3) and written to the wave's LDS region in MFMA
+//    fragment order, read back with one ds_read_b128 per fragment: a per-wave transpose,
+//    no workgroup barrier in the k loop.
 //  - W comes fragment-major (launch_frag_pack): one contiguous 1-KB load per 16-column x
 //    k-step fragment and plane.
 //  - Everything the epilogue reads (bias, LayerNorm vectors and statistics, residual) is
 //    loaded before the first store: a load issued after a store waits for it (vmcnt).
-// MFMA operands (16x16x32 bf16, or 16x16x4 f32 in four steps): row / column = lane & 15,
-// k = 8 g .. 8 g + 7 of the step (X3) or 4 g .. 4 g + 3 (fp32), g = lane >> 4.
-template <int BM, int BN, bool YT, int K1, bool S1, bool S2, bool X3, bool LOGITS>
+// MFMA operands: row / column = lane & 15, k = 8 g .. 8 g + 7 of the step (X3) or
+// 4 g .. 4 g + 3 (fp32), g = lane >> 4.
+template <int BM, int BN, bool YT, int K1, bool S1, bool S2, bool X3, bool LOGITS, int NW>
 __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c0, char* smem) {
-  using L = TileLds<BM, BN, YT, K1, X3>;
+  using L = TileLds<BM, BN, YT, K1, X3, NW>;
   constexpr int MF = BM / 16, NF = BN / 16;
   constexpr int KT = L::KT;
-  constexpr int KW = L::KW;
+  constexpr int KW = KT / NW;
   constexpr int KS = X3 ? 32 : 16;
   constexpr int NKS = KW / KS;
-  constexpr int NSEG = KW / 16;  // 64-byte segments of a row's K slice
+  constexpr int SPS = KS / 16;  // 64-byte row segments per k step
   static_assert(KW % KS == 0 && K1 % 32 == 0, "k steps never straddle A1 / A2");
   constexpr bool UV = S1 || (S2 && !YT);  // y tiles read A1 only; their LN2 residual uses 16-lane stats
   floatx4* uv_s = reinterpret_cast<floatx4*>(smem);                        // [2][KT / 4]
   char* a_s = smem + L::UV + (threadIdx.x >> 6) * L::AW;                   // this wave's fragments
-  float* red = reinterpret_cast<float*>(smem + L::UV + 4 * L::AW);        // [4][BM][BN + 1]
+  float* red = reinterpret_cast<float*>(smem + L::UV + NW * L::AW);       // [NW][BM][BN + 1]
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -154,11 +157,11 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
   const int ldw = YT ? K1 : K1 + kD;
   const int wt0 = (YT ? c0 : c0 - p.NY) / 16;  // first 16-column tile of W
 
-  // ---- every load first
+  // ---- every load first: k-vectors, statistics, then A and W step by step, epilogue operands
   floatx4 u4{}, v4{};
   const int kk4 = min(tid * 4, KT - 4);
   if constexpr (UV) {
-    static_assert(KT / 4 <= 256, "one float4 of u and of v per thread");
+    static_assert(KT / 4 <= 64 * NW, "one float4 of u and of v per thread");
     const bool in1 = kk4 < K1;
     const float* us = in1 ? (S1 ? p.a1_s + kk4 : p.a2_g) : (S2 ? p.a2_g + (kk4 - K1) : p.a2_g);
     const float* vs = in1 ? (S1 ? p.a1_c + kk4 : p.a2_b) : (S2 ? p.a2_b + (kk4 - K1) : p.a2_b);
@@ -174,32 +177,34 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
     if constexpr (S1) pa1[mf] = load_part4(p.a1_stats + (size_t)qrow[mf] * 2 * kSlices, c);
     if constexpr (S2 && !YT) pa2[mf] = load_part4(p.a2_stats + (size_t)qrow[mf] * 2 * kSlices, c);
   }
-  floatx4 ra[MF][NSEG];
+  floatx4 ra[NKS][SPS][MF];
+  floatx4 rw[NKS][NF][X3 ? 2 : 1];
 #pragma unroll
-  for (int mf = 0; mf < MF; ++mf)
+  for (int s = 0; s < NKS; ++s) {
 #pragma unroll
-    for (int sg = 0; sg < NSEG; ++sg) {
+    for (int h = 0; h < SPS; ++h) {
+      const int sg = s * SPS + h;
       const int k = kbeg + sg * 16 + c * 4;
       const bool in1 = kbeg + sg * 16 < K1;  // wave-uniform
-      ra[mf][sg] = *reinterpret_cast<const floatx4*>(in1 ? p.A1 + (size_t)qrow[mf] * K1 + k
-                                                           : p.A2 + (size_t)qrow[mf] * kD + (k - K1));
+#pragma unroll
+      for (int mf = 0; mf < MF; ++mf)
+        ra[s][h][mf] = *reinterpret_cast<const floatx4*>(in1 ? p.A1 + (size_t)qrow[mf] * K1 + k
+                                                             : p.A2 + (size_t)qrow[mf] * kD + (k - K1));
     }
-  floatx4 rw[NF][NKS][X3 ? 2 : 1];
 #pragma unroll
-  for (int nf = 0; nf < NF; ++nf)
-#pragma unroll
-    for (int s = 0; s < NKS; ++s) {
+    for (int nf = 0; nf < NF; ++nf) {
       const size_t fo = ((size_t)(wt0 + nf) * (ldw / KS) + kbeg / KS + s) * 64 + lane;
       if constexpr (X3) {
-        rw[nf][s][0] = reinterpret_cast<const floatx4*>(YT ? p.Fy_hi : p.Fz_hi)[fo];
-        rw[nf][s][1] = reinterpret_cast<const floatx4*>(YT ? p.Fy_lo : p.Fz_lo)[fo];
+        rw[s][nf][0] = reinterpret_cast<const floatx4*>(YT ? p.Fy_hi : p.Fz_hi)[fo];
+        rw[s][nf][1] = reinterpret_cast<const floatx4*>(YT ? p.Fy_lo : p.Fz_lo)[fo];
       } else {
-        rw[nf][s][0] = reinterpret_cast<const floatx4*>(YT ? p.Fy : p.Fz)[fo];
+        rw[s][nf][0] = reinterpret_cast<const floatx4*>(YT ? p.Fy : p.Fz)[fo];
       }
     }
-  // epilogue operands (row = tid >> 4 of each 16-row block, column = tid & 15 of each
-  // 16-column block)
-  const int erow = tid >> 4;
+  }
+  // epilogue operands (the first 256 threads: row = tid >> 4 of each 16-row block, column
+  // = tid & 15 of each 16-column block)
+  const int erow = (tid & 255) >> 4;
   const int ecol = tid & 15;
   float rres[YT ? MF : 1][YT ? NF : 1], ebias[NF], eg[YT && S2 ? NF : 1], eb[YT && S2 ? NF : 1];
   float2 est[YT && S2 ? MF : 1];
@@ -222,7 +227,6 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
     }
   }
 
-  // ---- A: transform, split, fragments to LDS
   if constexpr (UV) {
     if (tid * 4 < KT) {
       uv_s[kk4 / 4] = u4;
@@ -237,42 +241,9 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
     if constexpr (S1) merge_part4_quad(pa1[mf], c, m1[mf], rs1[mf]);
     if constexpr (S2 && !YT) merge_part4_quad(pa2[mf], c, m2[mf], rs2[mf]);
   }
-#pragma unroll
-  for (int mf = 0; mf < MF; ++mf)
-#pragma unroll
-    for (int sg = 0; sg < NSEG; ++sg) {
-      floatx4 x = ra[mf][sg];
-      const int kl = kbeg + sg * 16 + c * 4;  // the tile's k of x[0]
-      const bool in1 = kbeg + sg * 16 < K1;
-      if ((S1 && in1) || (S2 && !YT && !in1)) {
-        const floatx4 u = uv_s[kl / 4];
-        const floatx4 v = uv_s[KT / 4 + kl / 4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (in1) {
-            if constexpr (S1) x[e] = fmaxf(fmaf(rs1[mf], fmaf(-m1[mf], u[e], x[e]), v[e]), 0.f);
-          } else {
-            if constexpr (S2 && !YT) x[e] = fmaf((x[e] - m2[mf]) * rs2[mf], u[e], v[e]);
-          }
-        }
-      }
-      if constexpr (X3) {
-        // step sg / 2; k within the step (sg % 2) 16 + 4 c = 8 g_t + 4 (c & 1)
-        const int lt = q + 16 * ((sg & 1) * 2 + (c >> 1));
-        uint32_t h0, l0, h1, l1;
-        split2_bf16(x[0], x[1], h0, l0);
-        split2_bf16(x[2], x[3], h1, l1);
-        char* f = a_s + ((sg / 2) * MF + mf) * 2048 + lt * 16 + (c & 1) * 8;
-        *reinterpret_cast<uint2*>(f) = make_uint2(h0, h1);
-        *reinterpret_cast<uint2*>(f + 1024) = make_uint2(l0, l1);
-      } else {
-        const int lt = q + 16 * c;  // chunk sg; k within it 4 c
-        *reinterpret_cast<floatx4*>(a_s + (sg * MF + mf) * 1024 + lt * 16) = x;
-      }
-    }
-  __syncthreads();  // fragments in LDS (each wave reads its own; lanes cross)
 
-  // ---- MFMAs
+  // ---- k loop: transform + split step s's A pieces into the wave's LDS fragments, read
+  // them back in MFMA order, MFMAs with the step's W fragments
   floatx4 acc[MF][NF];
 #pragma unroll
   for (int mf = 0; mf < MF; ++mf)
@@ -280,35 +251,74 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
     for (int nf = 0; nf < NF; ++nf) acc[mf][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < NKS; ++s) {
+#pragma unroll
+    for (int h = 0; h < SPS; ++h) {
+      const int sg = s * SPS + h;
+      const int kl = kbeg + sg * 16 + c * 4;  // the tile's k of the piece's first value
+      const bool in1 = kbeg + sg * 16 < K1;
+      floatx4 uu{}, vv{};
+      if ((S1 && in1) || (S2 && !YT && !in1)) {
+        uu = uv_s[kl / 4];
+        vv = uv_s[KT / 4 + kl / 4];
+      }
+#pragma unroll
+      for (int mf = 0; mf < MF; ++mf) {
+        floatx4 x = ra[s][h][mf];
+        if ((S1 && in1) || (S2 && !YT && !in1)) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (in1) {
+              if constexpr (S1) x[e] = fmaxf(fmaf(rs1[mf], fmaf(-m1[mf], uu[e], x[e]), vv[e]), 0.f);
+            } else {
+              if constexpr (S2 && !YT) x[e] = fmaf((x[e] - m2[mf]) * rs2[mf], uu[e], vv[e]);
+            }
+          }
+        }
+        if constexpr (X3) {
+          // k within the step h 16 + 4 c = 8 g_t + 4 (c & 1)
+          const int lt = q + 16 * (h * 2 + (c >> 1));
+          uint32_t h0, l0, h1, l1;
+          split2_bf16(x[0], x[1], h0, l0);
+          split2_bf16(x[2], x[3], h1, l1);
+          char* f = a_s + mf * 2048 + lt * 16 + (c & 1) * 8;
+          *reinterpret_cast<uint2*>(f) = make_uint2(h0, h1);
+          *reinterpret_cast<uint2*>(f + 1024) = make_uint2(l0, l1);
+        } else {
+          *reinterpret_cast<floatx4*>(a_s + mf * 1024 + (q + 16 * c) * 16) = x;  // k within the step 4 c
+        }
+      }
+    }
     if constexpr (X3) {
       bf16x8 ah[MF], al[MF];
 #pragma unroll
       for (int mf = 0; mf < MF; ++mf) {
-        const char* f = a_s + (s * MF + mf) * 2048 + lane * 16;
+        const char* f = a_s + mf * 2048 + lane * 16;
         ah[mf] = *reinterpret_cast<const bf16x8*>(f);
         al[mf] = *reinterpret_cast<const bf16x8*>(f + 1024);
       }
+      // the three passes over all MF x NF accumulators in turn (independent MFMAs between
+      // two that update one accumulator; the per-element order hi*hi, hi*lo, lo*hi is kept)
 #pragma unroll
-      for (int mf = 0; mf < MF; ++mf)
+      for (int pass = 0; pass < 3; ++pass)
 #pragma unroll
-        for (int nf = 0; nf < NF; ++nf) {
-          const bf16x8 bh = __builtin_bit_cast(bf16x8, rw[nf][s][0]);
-          const bf16x8 bl = __builtin_bit_cast(bf16x8, rw[nf][s][1]);
-          acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mf], bh, acc[mf][nf], 0, 0, 0);
-          acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mf], bl, acc[mf][nf], 0, 0, 0);
-          acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[mf], bh, acc[mf][nf], 0, 0, 0);
-        }
+        for (int mf = 0; mf < MF; ++mf)
+#pragma unroll
+          for (int nf = 0; nf < NF; ++nf) {
+            const bf16x8 a = pass == 2 ? al[mf] : ah[mf];
+            const bf16x8 b = __builtin_bit_cast(bf16x8, rw[s][nf][pass == 1 ? 1 : 0]);
+            acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[mf][nf], 0, 0, 0);
+          }
     } else {
       floatx4 a[MF];
 #pragma unroll
-      for (int mf = 0; mf < MF; ++mf) a[mf] = *reinterpret_cast<const floatx4*>(a_s + (s * MF + mf) * 1024 + lane * 16);
+      for (int mf = 0; mf < MF; ++mf) a[mf] = *reinterpret_cast<const floatx4*>(a_s + mf * 1024 + lane * 16);
 #pragma unroll
-      for (int mf = 0; mf < MF; ++mf)
+      for (int e = 0; e < 4; ++e)
 #pragma unroll
-        for (int nf = 0; nf < NF; ++nf)
+        for (int mf = 0; mf < MF; ++mf)
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mf][e], rw[nf][s][0][e], acc[mf][nf], 0, 0, 0);
+          for (int nf = 0; nf < NF; ++nf)
+            acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mf][e], rw[s][nf][0][e], acc[mf][nf], 0, 0, 0);
     }
   }
 
@@ -322,7 +332,7 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
 #pragma unroll
       for (int r = 0; r < 4; ++r) red[(wave * BM + mf * 16 + g * 4 + r) * (BN + 1) + nf * 16 + li] = acc[mf][nf][r];
   __syncthreads();
-  if (dec_skip(p.st, p.t)) return;
+  if (tid >= 256 || dec_skip(p.st, p.t)) return;
 #pragma unroll
   for (int mf = 0; mf < MF; ++mf) {
     const int orow = r0 + mf * 16 + erow;
@@ -331,8 +341,9 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
 #pragma unroll
     for (int nf = 0; nf < NF; ++nf) {
       const int lr = mf * 16 + erow, lc = nf * 16 + ecol;
-      const float val = ((red[(0 * BM + lr) * (BN + 1) + lc] + red[(1 * BM + lr) * (BN + 1) + lc]) +
-                         red[(2 * BM + lr) * (BN + 1) + lc]) + red[(3 * BM + lr) * (BN + 1) + lc];
+      float val = red[lr * (BN + 1) + lc];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) val += red[(w * BM + lr) * (BN + 1) + lc];
       const int ocol = c0 + nf * 16 + ecol;
       if constexpr (YT) {
         float res = rres[mf][nf];
@@ -381,24 +392,24 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
   }
 }
 
-template <int BM, int BN, int K1, bool S1, bool S2, bool X3, bool LOGITS>
-__global__ void __launch_bounds__(256) foldwide_kernel(FoldGemmParams p) {
-  constexpr int BYTES = LOGITS ? TileLds<BM, BN, false, 0, X3>::BYTES
-                               : (TileLds<BM, BN, true, K1, X3>::BYTES > TileLds<BM, BN, false, K1, X3>::BYTES
-                                      ? TileLds<BM, BN, true, K1, X3>::BYTES
-                                      : TileLds<BM, BN, false, K1, X3>::BYTES);
+template <int BM, int BN, int K1, bool S1, bool S2, bool X3, bool LOGITS, int NW>
+__global__ void __launch_bounds__(64 * NW) foldwide_kernel(FoldGemmParams p) {
+  constexpr int BYTES = LOGITS ? TileLds<BM, BN, false, 0, X3, NW>::BYTES
+                               : (TileLds<BM, BN, true, K1, X3, NW>::BYTES > TileLds<BM, BN, false, K1, X3, NW>::BYTES
+                                      ? TileLds<BM, BN, true, K1, X3, NW>::BYTES
+                                      : TileLds<BM, BN, false, K1, X3, NW>::BYTES);
   __shared__ __attribute__((aligned(16))) char smem[BYTES];
   const int ncol = (p.NY + p.NZ) / BN;
   const int b = blockIdx.x;
   const int c0 = (b % ncol) * BN;
   const int r0 = (b / ncol) * BM;
   if constexpr (LOGITS) {
-    wide_tile<BM, BN, false, 0, false, true, X3, true>(p, r0, c0, smem);
+    wide_tile<BM, BN, false, 0, false, true, X3, true, NW>(p, r0, c0, smem);
   } else {
     if (c0 < p.NY)
-      wide_tile<BM, BN, true, K1, S1, S2, X3, false>(p, r0, c0, smem);
+      wide_tile<BM, BN, true, K1, S1, S2, X3, false, NW>(p, r0, c0, smem);
     else
-      wide_tile<BM, BN, false, K1, S1, S2, X3, false>(p, r0, c0, smem);
+      wide_tile<BM, BN, false, K1, S1, S2, X3, false, NW>(p, r0, c0, smem);
   }
 }
 
@@ -428,24 +439,36 @@ __global__ void frag_pack_kernel(const float* __restrict__ W, int N, int K, uint
   }
 }
 
-template <int BM, int BN, bool X3, bool LOGITS>
-void launch_fw(const FoldGemmParams& p, hipStream_t s) {
+template <int BM, int BN, bool X3, bool LOGITS, int NW>
+void launch_fw_nw(const FoldGemmParams& p, hipStream_t s) {
   const int ncol = (p.NY + p.NZ) / BN;
   const dim3 grid(ncol * ((p.B + BM - 1) / BM));
   if constexpr (LOGITS) {
-    foldwide_kernel<BM, BN, 0, false, true, X3, true><<<grid, 256, 0, s>>>(p);
+    foldwide_kernel<BM, BN, 0, false, true, X3, true, NW><<<grid, 64 * NW, 0, s>>>(p);
   } else {
     const bool s1 = p.a1_stats != nullptr, s2 = p.a2_stats != nullptr;
     if (p.K1 == 256 && !s1 && !s2) {
-      foldwide_kernel<BM, BN, 256, false, false, X3, false><<<grid, 256, 0, s>>>(p);
+      foldwide_kernel<BM, BN, 256, false, false, X3, false, NW><<<grid, 64 * NW, 0, s>>>(p);
     } else if (p.K1 == 256 && !s1 && s2) {
-      foldwide_kernel<BM, BN, 256, false, true, X3, false><<<grid, 256, 0, s>>>(p);
+      foldwide_kernel<BM, BN, 256, false, true, X3, false, NW><<<grid, 64 * NW, 0, s>>>(p);
     } else if (p.K1 == 512 && s1 && s2) {
-      foldwide_kernel<BM, BN, 512, true, true, X3, false><<<grid, 256, 0, s>>>(p);
+      foldwide_kernel<BM, BN, 512, true, true, X3, false, NW><<<grid, 64 * NW, 0, s>>>(p);
     } else {
       throw std::runtime_error("foldwide: built for (K1 256, A2 plain or LayerNorm), (K1 512, both), logits");
     }
   }
+}
+
+// NW waves split K (p.waves: 4 or 8; 0 = kWideWaves).  The same NW at every row count, so
+// a row's k order never depends on its chain's length.
+// measured (tools/wide_bench, profiles/r03/wide_bench_v3.log): 8 waves for the fold GEMMs
+// (FFN at 256 rows 9.1 -> 7.5 us), 4 for the logits (10.8 vs 11.8 us)
+template <int BM, int BN, bool X3, bool LOGITS>
+void launch_fw(const FoldGemmParams& p, hipStream_t s) {
+  if ((p.waves ? p.waves : (LOGITS ? 4 : 8)) == 8)
+    launch_fw_nw<BM, BN, X3, LOGITS, 8>(p, s);
+  else
+    launch_fw_nw<BM, BN, X3, LOGITS, 4>(p, s);
 }
 
 }  // namespace
@@ -460,6 +483,7 @@ void launch_foldwide(const FoldGemmParams& p, hipStream_t s) {
   } else {
     if (p.NY != kD || p.NZ % 32 != 0 || (p.NZ && (!p.bz || !p.z)))
       throw std::runtime_error("foldwide: NY == d and NZ a multiple of 32 with bz, z");
+    // XCD placement (column tile = block % ncol, ncol % 8 == 0) holds for 16- and 32-wide tiles
     if (!p.A1 || !p.A2 || !p.by || !p.y || !p.y_stats) throw std::runtime_error("foldwide: null operand");
   }
   if ((p.a1_stats && (!p.a1_s || !p.a1_c)) || (p.a2_stats && (!p.a2_g || !p.a2_b)))
@@ -470,12 +494,35 @@ void launch_foldwide(const FoldGemmParams& p, hipStream_t s) {
   if (!have) throw std::runtime_error("foldwide: fragment-major weights (launch_frag_pack) missing");
   if (p.B <= 0) return;
   // fold GEMMs: 16-row tiles up to 64 rows (more workgroups for a short chain), 32 above
-  if (logits) {  // 16-row tiles at every R: fc_out's 159 column tiles x R / 16 fill the chip
-    if (x3) launch_fw<16, 32, true, true>(p, s); else launch_fw<16, 32, false, true>(p, s);
-  } else if (p.B <= 64) {
-    if (x3) launch_fw<16, 32, true, false>(p, s); else launch_fw<16, 32, false, false>(p, s);
+  if (logits) {  // 16-row tiles; columns per tile p.tile_cols (A/B) or the default below
+    // 64-column tiles above 64 rows (9.9 vs 10.9 us at 256 rows), 32 up to 64 (5.2 vs 5.9 us);
+    // a row's k order does not depend on the tile width (profiles/r03/wide_bench_v4.log)
+    const int bn = p.tile_cols ? p.tile_cols : (p.B > 64 ? 64 : 32);
+    if (p.NZ % bn != 0) throw std::runtime_error("foldwide logits: NZ must be a multiple of the column tile");
+    if (bn == 128) {
+      if (x3) launch_fw<16, 128, true, true>(p, s); else launch_fw<16, 128, false, true>(p, s);
+    } else if (bn == 64) {
+      if (x3) launch_fw<16, 64, true, true>(p, s); else launch_fw<16, 64, false, true>(p, s);
+    } else {
+      if (x3) launch_fw<16, 32, true, true>(p, s); else launch_fw<16, 32, false, true>(p, s);
+    }
   } else {
-    if (x3) launch_fw<32, 32, true, false>(p, s); else launch_fw<32, 32, false, false>(p, s);
+    // 16-column tiles when 32-column ones would leave CUs idle (e.g. N = 512 at 256 rows)
+    const int bm = p.B <= 64 ? 16 : 32;
+    const bool narrow_n = (p.NY + p.NZ) / 32 * ((p.B + bm - 1) / bm) < 256;
+    if (bm == 16) {
+      if (narrow_n) {
+        if (x3) launch_fw<16, 16, true, false>(p, s); else launch_fw<16, 16, false, false>(p, s);
+      } else {
+        if (x3) launch_fw<16, 32, true, false>(p, s); else launch_fw<16, 32, false, false>(p, s);
+      }
+    } else {
+      if (narrow_n) {
+        if (x3) launch_fw<32, 16, true, false>(p, s); else launch_fw<32, 16, false, false>(p, s);
+      } else {
+        if (x3) launch_fw<32, 32, true, false>(p, s); else launch_fw<32, 32, false, false>(p, s);
+      }
+    }
   }
   MOCR_HIP_CHECK(hipGetLastError());
 }

@@ -668,7 +668,7 @@ struct mocr_engine {
     lay.reset(new Layout(cfg));
 
     const size_t B = cfg.max_batch;
-    Vpad = (cfg.vocab + 31) / 32 * 32;  // whole 32-column logits tiles (decwide.hip)
+    Vpad = (cfg.vocab + 127) / 128 * 128;  // whole logits tiles of up to 128 columns (decwide.hip)
     const size_t d = cfg.d_model, L = cfg.n_layers;
     if (cfg.arch == MOCR_ARCH_RES18TRANS) {
       init_res18();

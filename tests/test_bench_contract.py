@@ -52,11 +52,21 @@ def test_attention_roofline_is_the_dominant_attention_class(bench):
 
 
 def test_decode_roofline_against_hbm(bench):
-    r = bench.roofline_decode(stats(), "bf16x3")
+    r = bench.roofline_decode(stats(), "bf16x3", 64, 128)
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
-    assert r["achieved"] == pytest.approx(247.1e6 / 0.2435e-3 / 1e9)
+    # SURVEY §8(d) at B = 64, bf16: weights 13.2 MB + cross K/V 75.5 MB + self K/V <= 67 MB per step
+    survey = sum(bench.survey_decode_step_bytes(64, t) for t in range(128)) / 128
+    assert bench.survey_decode_step_bytes(64, 0) == pytest.approx(13.08e6 + 75.50e6 + 1.05e6, rel=1e-3)
+    assert r["algorithmic_bytes_per_step"] == pytest.approx(survey)
+    assert r["achieved"] == pytest.approx(survey / 0.2435e-3 / 1e9)
     assert r["frac"] == pytest.approx(r["achieved"] / 8000.0)
-    assert bench.roofline_decode({}, "bf16x3") is None
+    assert r["as_built_achieved"] == pytest.approx(247.1e6 / 0.2435e-3 / 1e9)
+    assert bench.roofline_decode({}, "bf16x3", 64, 128) is None
+
+
+def test_e2e_roofline_is_baseline_md_section4(bench):
+    # 1 / (26.39 GFLOP / 2.5 PF + 245 MB / 8 TB/s) ~ 24.3k img/s per GPU
+    assert bench.E2E_ROOFLINE_IMG_S == pytest.approx(24.3e3, rel=0.01)
 
 
 def test_committed_pmc_traffic_covers_the_roofline_classes(bench):
@@ -70,4 +80,8 @@ def test_default_run_is_one_gpu_minutes_scale(bench, monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py"])
     a = bench.parse()
     assert a.gpus == 1 and a.steps == 64 and a.warmup == 3 and a.batch == 64 and a.tokens == 128
-    assert a.replicas == 4 and a.precision == "bf16x3" and a.image == [384, 384]
+    assert a.chain == 4 and a.replicas == 2 and a.precision == "bf16x3" and a.image == [384, 384]
+    assert a.cpu_sample == 64 and a.cpu_runs == 3  # B = 64, median of 3
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--arch", "res18trans"])
+    a = bench.parse()
+    assert a.chain == 1 and a.replicas == 4  # its encoder attends across its batch of 64

@@ -66,7 +66,7 @@ def check_teacher_forced(eng, ref_ids, margins, tie, ref_logits):
 
 # rows of the 64 that equal the fixture over all 129 columns, near-tie rows included
 # (measured on MI355X); a floor so that a regression cannot pass silently
-C2_ROWS_EQUAL_FLOOR = {"bf16x3": 61, "fp32": 61}
+C2_ROWS_EQUAL_FLOOR = {"bf16x3": 64, "fp32": 64}
 
 
 @pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
@@ -106,6 +106,8 @@ def test_config5_res18trans_b64_greedy128(pkg, golden):
     rec = {"config": "C5", "precision": "bf16x3"}
     n_full = check_ids(res.ids, g["ids"], g["margins"], tie=2e-4, record=rec)
     assert n_full >= 56, n_full
+    # every row but row 42 (an exact fp32 tie at step 42) equals the fixture in full
+    assert rec["rows_equal_all_columns"] >= 63, rec
     check_teacher_forced(eng, g["ids"], g["margins"], 2e-4, g["logits"])
     eng.close()
 

@@ -19,11 +19,12 @@ ap.add_argument("--steps", type=int, default=12)
 ap.add_argument("--precision", default="bf16x3")
 ap.add_argument("--modes", default="encode,decode,both")
 ap.add_argument("--lib", default=None, help="libmathocr.so to load (an A/B build from tools/build_variant.sh)")
+ap.add_argument("--rows", type=int, default=64, help="images per engine call (decode chain rows)")
 a = ap.parse_args()
 pkg = importlib.import_module("handwritten-math-ocr-api_amd")
 if a.lib:
     pkg.engine.load_library(a.lib)
-B, S = 64, 128
+B, S = a.rows, 128
 pool = pkg.pipeline.ReplicaPool(a.replicas, img_hw=(384, 384), max_batch=B, precision=a.precision, device=0)
 pool.load_weights(pkg.synth.make_weights(1234, "init"))
 for i, e in enumerate(pool.engines):
@@ -45,7 +46,7 @@ def both(e, k):
     dec(e, k)
 
 
-out = {"replicas": a.replicas, "lib": a.lib or "default"}
+out = {"replicas": a.replicas, "rows": B, "lib": a.lib or "default"}
 for name, fn in (("encode", enc), ("decode", dec), ("both", both)):
     if name not in a.modes.split(","):
         continue

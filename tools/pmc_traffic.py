@@ -43,7 +43,7 @@ def classes_in_order(mlp_fused=(), attn_fused=(), attn_noproj=()):
 def main(fetch_csv, write_csv, out, decode_steps=0):
     decode_steps = int(decode_steps)
     # engine dispatches only (the load-time decoder weight folding is not an encoder kernel)
-    keep = lambda r: "mocr" in r["Kernel_Name"] and "fold_mm" not in r["Kernel_Name"]
+    keep = lambda r: "mocr" in r["Kernel_Name"] and "fold_mm" not in r["Kernel_Name"] and "frag_pack" not in r["Kernel_Name"]
     f = [r for r in csv.DictReader(open(fetch_csv)) if keep(r)]
     w = [r for r in csv.DictReader(open(write_csv)) if keep(r)]
     assert len(f) == len(w)

@@ -70,7 +70,7 @@ int main(int argc, char** argv) {
   std::vector<int> Rs;
   for (int i = 1; i < argc; ++i) Rs.push_back(atoi(argv[i]));
   if (Rs.empty()) Rs = {64, 256};
-  const int d = 256, P = 150, M = 144, Vp = 5088, V = 5075, t = 100;
+  const int d = 256, P = 150, M = 144, Vp = 5120, V = 5075, t = 100;
   const int Rmax = 512;
   float* a1 = alloc<float>((size_t)Rmax * 512);
   float* a2 = alloc<float>((size_t)Rmax * d);
@@ -104,9 +104,10 @@ int main(int argc, char** argv) {
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   for (int R : Rs) {
-    auto fg = [&](int K1, int NZ, bool s1, bool s2, bool wide, bool x3) {
+    auto fg = [&](int K1, int NZ, bool s1, bool s2, bool wide, bool x3, int nw = 0) {
       return [=](hipStream_t ss) {
         FoldGemmParams p{};
+        p.waves = nw;
         p.B = R; p.t = t; p.A1 = a1; p.K1 = K1; p.A2 = a2;
         if (s2) { p.a2_stats = st2; p.a2_g = vec; p.a2_b = vec; }
         if (s1) { p.a1_stats = st1; p.a1_s = vec; p.a1_c = vec; }
@@ -117,10 +118,12 @@ int main(int argc, char** argv) {
         if (wide) launch_foldwide(p, ss); else launch_foldgemm(p, ss);
       };
     };
-    auto lg = [&](bool wide, bool x3) {
+    auto lg = [&](bool wide, bool x3, int nw = 0, int bm = 0) {
       return [=](hipStream_t ss) {
         if (wide) {
           FoldGemmParams p{};
+          p.waves = nw;
+          p.tile_cols = bm;
           p.B = R; p.t = t; p.K1 = 0; p.NY = 0; p.A2 = a2; p.a2_stats = st2; p.a2_g = vec; p.a2_b = vec;
           p.Wz = W; p.bz = bias; p.z = z; p.NZ = Vp; p.n_valid = V; p.part = part;
           if (x3) { p.Fz_hi = Wh; p.Fz_lo = Wh; }
@@ -151,15 +154,22 @@ int main(int argc, char** argv) {
     };
     std::vector<std::pair<std::string, std::function<void(hipStream_t)>>> cases = {
         {"narrow y256+z256 K1=256 LN x3", fg(256, 256, false, true, false, true)},
-        {"wide   y256+z256 K1=256 LN x3", fg(256, 256, false, true, true, true)},
+        {"wide4  y256+z256 K1=256 LN x3", fg(256, 256, false, true, true, true, 4)},
+        {"wide8  y256+z256 K1=256 LN x3", fg(256, 256, false, true, true, true, 8)},
         {"narrow y256+z512 K1=256 LN x3", fg(256, 512, false, true, false, true)},
-        {"wide   y256+z512 K1=256 LN x3", fg(256, 512, false, true, true, true)},
+        {"wide4  y256+z512 K1=256 LN x3", fg(256, 512, false, true, true, true, 4)},
+        {"wide8  y256+z512 K1=256 LN x3", fg(256, 512, false, true, true, true, 8)},
         {"narrow y256+z768 K1=512 unf x3", fg(512, 768, true, true, false, true)},
-        {"wide   y256+z768 K1=512 unf x3", fg(512, 768, true, true, true, true)},
-        {"wide   y256+z768 K1=512 unf f32", fg(512, 768, true, true, true, false)},
+        {"wide4  y256+z768 K1=512 unf x3", fg(512, 768, true, true, true, true, 4)},
+        {"wide8  y256+z768 K1=512 unf x3", fg(512, 768, true, true, true, true, 8)},
+        {"wide8  y256+z768 K1=512 unf f32", fg(512, 768, true, true, true, false, 8)},
         {"narrow logits f32", lg(false, false)},
-        {"wide   logits f32", lg(true, false)},
-        {"wide   logits x3", lg(true, true)},
+        {"wide4  logits x3", lg(true, true, 4)},
+        {"wide8  logits x3", lg(true, true, 8)},
+        {"wide4  logits x3 64-col tiles", lg(true, true, 4, 64)},
+        {"wide4  logits x3 128-col tiles", lg(true, true, 4, 128)},
+        {"wide8  logits x3 128-col tiles", lg(true, true, 8, 128)},
+        {"wide8  logits f32", lg(true, false, 8)},
         {"fold cross-attn M=144", fa(false)},
         {"fold self-attn t=100", fa(true)},
     };
