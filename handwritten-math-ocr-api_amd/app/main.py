@@ -8,11 +8,14 @@ Routes and payloads follow the reference:
 
 Differences, all on the compute side:
 
-- ``/predict/batch`` decodes every valid image of the request as ONE batch on the GPU. The reference loops image by image. Per-image results are unchanged; see ``im2latex.predict_batch``.
+- ``/predict/batch`` decodes every valid image of the request as ONE batch on the GPU. The reference loops image by image. Per-image results are unchanged; see ``im2latex.predict_batch``. If the batched call fails, each image is retried alone, so only the images that fail on their own are reported ``success: false`` (the reference's per-image error isolation, :562-570).
 - Engine calls run in a worker thread. The reference calls the model synchronously on the event loop (:486). ctypes releases the GIL, and a lock serialises calls on the one engine.
+- ``/metrics`` adds the engine's images/s and a histogram of engine-call latencies to the reference's keys.
 
 Rate limiting, API keys, CORS and cloud logging are product policy, not the hot path, and
-are not rebuilt.
+are not rebuilt: ``/health`` reports ``rate_limiter_initialized: false``
+and does not count it, ``/metrics`` reports the rate limiter as not available, as the
+reference does when its limiter is missing.
 """
 from __future__ import annotations
 
@@ -111,23 +114,30 @@ def _decode_image(data: bytes):
         raise HTTPException(status_code=400, detail="Invalid image data") from e
 
 
+# engine-call latency histogram bucket bounds (ms), Prometheus-style cumulative counts
+LATENCY_BUCKETS_MS = (5, 10, 25, 50, 100, 250, 500, 1000, 2500)
+
+
 class State:
     """Model state of one server process (the reference keeps module globals)."""
 
     def __init__(self, engine=None, vocab=None, idx2char=None, predictor: Optional[Callable] = None,
-                 device: str = "cuda:0"):
+                 device: str = "cuda:0", model_dir: Optional[str] = None, checkpoint: str = "model.pth"):
         self.engine = engine
         self.vocab = vocab
         self.idx2char = idx2char
         self.predictor = predictor or (lambda imgs: im2latex.predict_batch(self.engine, imgs, self.vocab,
                                                                             self.idx2char))
         self.device = device
+        self.model_dir = model_dir
+        self.checkpoint = checkpoint
         self.lock = threading.Lock()
         self.start = time.time()
         self.load_time: Optional[float] = None
         self.predictions = 0
         self.images_done = 0
         self.gpu_seconds = 0.0
+        self.latency_counts = [0] * (len(LATENCY_BUCKETS_MS) + 1)
 
     @property
     def loaded(self):
@@ -137,9 +147,21 @@ class State:
         with self.lock:
             t0 = time.time()
             out = self.predictor(images)
-            self.gpu_seconds += time.time() - t0
+            dt = time.time() - t0
+            self.gpu_seconds += dt
             self.images_done += images.shape[0]
+            ms = dt * 1e3
+            self.latency_counts[next((i for i, b in enumerate(LATENCY_BUCKETS_MS) if ms <= b),
+                                     len(LATENCY_BUCKETS_MS))] += 1
             return out
+
+    def device_available(self) -> bool:
+        if self.engine is None:
+            return self.predictor is not None  # injected predictor (tests): no device to check
+        try:
+            return self.engine.lib.mocr_device_count() > self.engine.device
+        except Exception:  # noqa: BLE001
+            return False
 
 
 def load_state(model_dir: str, device: str = "cuda:0", precision: str = "bf16x3") -> State:
@@ -152,7 +174,7 @@ def load_state(model_dir: str, device: str = "cuda:0", precision: str = "bf16x3"
     if ckpt is None:
         raise FileNotFoundError(f"no checkpoint in {model_dir}")
     eng = im2latex.load_model(ckpt, vocab, device, precision=precision)
-    st = State(eng, vocab, idx2char, device=device)
+    st = State(eng, vocab, idx2char, device=device, model_dir=model_dir, checkpoint=os.path.basename(ckpt))
     st.load_time = time.time() - t0
     return st
 
@@ -160,6 +182,7 @@ def load_state(model_dir: str, device: str = "cuda:0", precision: str = "bf16x3"
 def create_app(state: Optional[State] = None, model_dir: Optional[str] = None) -> FastAPI:
     app = FastAPI(title=API_TITLE, version=API_VERSION)
     holder = {"state": state}
+    app_start = time.time()
 
     def get_state() -> State:
         if holder["state"] is None:
@@ -214,10 +237,19 @@ def create_app(state: Optional[State] = None, model_dir: Optional[str] = None) -
         if tensors:
             try:
                 preds = await run_in_threadpool(st.run, np.concatenate(tensors, 0))
-            except Exception as e:  # noqa: BLE001
-                raise HTTPException(status_code=500, detail=f"Batch prediction failed: {e}") from e
-            for i, (formula, confidence) in zip(ok_idx, preds):
-                results[i] = {"index": i, "formula": formula, "confidence": confidence, "success": True}
+            except Exception:  # noqa: BLE001 - isolate the failing images (reference :562-570)
+                preds = []
+                for t in tensors:
+                    try:
+                        preds.append((await run_in_threadpool(st.run, t))[0])
+                    except Exception as e:  # noqa: BLE001
+                        preds.append(e)
+            for i, pr in zip(ok_idx, preds):
+                if isinstance(pr, Exception):
+                    results[i] = {"index": i, "formula": "", "confidence": None, "success": False, "error": str(pr)}
+                else:
+                    formula, confidence = pr
+                    results[i] = {"index": i, "formula": formula, "confidence": confidence, "success": True}
         st.predictions += len(req.images)
         ok = sum(1 for r in results if r["success"])
         return BatchPredictionResponse(results=results, total_images=len(req.images), successful_predictions=ok,
@@ -235,29 +267,65 @@ def create_app(state: Optional[State] = None, model_dir: Optional[str] = None) -
 
     @app.get("/health", response_model=HealthResponse)
     async def health():
+        """Reference keys (:613-649); the rate limiter is not rebuilt."""
         st = holder["state"]
+        mdir = (st.model_dir if st else None) or model_dir
+        files = {}
+        if mdir:
+            ckpt = st.checkpoint if st else "model.pth"
+            files = {ckpt: os.path.exists(os.path.join(mdir, ckpt)),
+                     "vocab.json": os.path.exists(os.path.join(mdir, "vocab.json"))}
         checks = {"model_loaded": bool(st and st.loaded),
-                  "vocab_loaded": bool(st and st.vocab is not None)}
-        return HealthResponse(healthy=all(checks.values()), checks=checks, timestamp=_now())
+                  "vocab_loaded": bool(st and st.vocab is not None and st.idx2char is not None),
+                  "device_available": bool(st and st.device_available()),
+                  "rate_limiter_initialized": False,
+                  "model_files_exist": files,
+                  "environment": os.environ.get("ENVIRONMENT", "production")}
+        healthy = (checks["model_loaded"] and checks["vocab_loaded"] and checks["device_available"]
+                   and all(files.values()))
+        return HealthResponse(healthy=healthy, checks=checks, timestamp=_now())
 
     @app.get("/model/info")
     async def model_info():
+        """Reference keys (:651-673); 503 until the model is loaded."""
         st = holder["state"]
-        eng = st.engine if st else None
-        return {"model_type": "Swin-T encoder + 8-layer Transformer decoder (greedy)",
-                "vocab_size": len(st.vocab) if st and st.vocab else None,
-                "image_size": [config.img_h, config.img_w], "max_sequence_length": config.max_seq_len,
-                "engine": {"precision": eng.precision, "max_batch": eng.max_batch} if eng is not None else None}
+        if st is None or not st.loaded:
+            raise HTTPException(status_code=503, detail="Model not loaded")
+        eng = st.engine
+        return {"model_config": {"img_height": config.img_h, "img_width": config.img_w, "d_model": config.d_model,
+                                 "num_heads": config.nhead, "num_decoder_layers": config.num_decoder_layers,
+                                 "dim_feedforward": config.dim_feedforward, "dropout": config.dropout,
+                                 "max_seq_len": config.max_seq_len},
+                "vocab_info": {"vocab_size": len(st.vocab) if st.vocab else 0,
+                               "special_tokens": config.special_tokens},
+                "device": st.device,
+                # the engine's weights: the parameters the forward pass uses (the reference
+                # also counts the registered but unused swin.norm / swin.head, SURVEY.md K3)
+                "model_parameters": eng.weight_count() if eng is not None else 0,
+                "engine": {"precision": eng.precision, "max_batch": eng.max_batch,
+                           "arch": eng.arch} if eng is not None else None}
 
     @app.get("/metrics")
     async def metrics():
+        """Reference keys (:675-702) plus the engine's throughput and call latencies."""
+        import psutil
         st = holder["state"]
-        if st is None:
-            return {"total_predictions": 0}
-        return {"total_predictions": st.predictions, "images_processed": st.images_done,
-                "engine_seconds": st.gpu_seconds,
-                "images_per_engine_second": st.images_done / st.gpu_seconds if st.gpu_seconds else None,
-                "uptime": time.time() - st.start}
+        uptime = time.time() - (st.start if st else app_start)
+        total = st.predictions if st else 0
+        out = {"predictions": {"total": total, "rate_per_second": total / uptime if uptime > 0 else 0},
+               "system": {"cpu_percent": psutil.cpu_percent(), "memory_percent": psutil.virtual_memory().percent,
+                          "disk_percent": psutil.disk_usage("/").percent},
+               "rate_limiter": {"error": "Rate limiter not available"},
+               "uptime_seconds": uptime}
+        if st is not None:
+            cum, buckets = 0, {}
+            for b, n in zip(list(LATENCY_BUCKETS_MS) + ["+Inf"], st.latency_counts):
+                cum += n
+                buckets[f"le_{b}"] = cum
+            out["engine"] = {"images_processed": st.images_done, "engine_seconds": st.gpu_seconds,
+                             "images_per_engine_second": st.images_done / st.gpu_seconds if st.gpu_seconds else None,
+                             "call_latency_ms_histogram": buckets}
+        return out
 
     return app
 

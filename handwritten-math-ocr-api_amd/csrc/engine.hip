@@ -1783,6 +1783,16 @@ extern "C" {
 
 int mocr_abi_version(void) { return MOCR_ABI_VERSION; }
 
+int mocr_device_count(void) {
+  int n = 0;
+  const hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    g_last_error = std::string("hipGetDeviceCount: ") + hipGetErrorString(e);
+    return -1000 - (int)e;
+  }
+  return n;
+}
+
 size_t mocr_weight_count(const mocr_config* cfg) {
   try {
     check_config(*cfg);

@@ -51,12 +51,19 @@ def load_library(path: str = LIB_PATH):
     if not os.path.exists(path):
         raise RuntimeError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = ctypes.CDLL(path)
+    lib.mocr_source_hash.restype = ctypes.c_char_p
+    lib.mocr_source_hash.argtypes = []
+    want = source_hash()
+    if want is not None and lib.mocr_source_hash().decode() != want:
+        raise RuntimeError(f"{path} was built from other sources (hash {lib.mocr_source_hash().decode()}, "
+                           f"sources {want}): rebuild it with `python -c 'import __graft_entry__ as g; g.build()'`")
     P, I, SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
     i32p = ctypes.POINTER(ctypes.c_int32)
     f32p = ctypes.POINTER(ctypes.c_float)
     cfgp = ctypes.POINTER(MocrConfig)
     sigs = {
         "mocr_abi_version": (I, []),
+        "mocr_device_count": (I, []),
         "mocr_weight_count": (SZ, [cfgp]),
         "mocr_memory_tokens": (I, [cfgp]),
         "mocr_create": (I, [cfgp, I, ctypes.POINTER(P)]),
@@ -91,8 +98,25 @@ def load_library(path: str = LIB_PATH):
     return lib
 
 
+def source_hash():
+    """sha256 (16 hex digits) of the sources the Makefile bakes into libmathocr.so
+    (csrc/*.hip and csrc/*.h sorted, then include/mathocr.h), or None without sources."""
+    import glob
+    import hashlib
+    files = sorted(glob.glob(os.path.join(_HERE, "csrc", "*.hip")) + glob.glob(os.path.join(_HERE, "csrc", "*.h")),
+                   key=os.path.basename)
+    hdr = os.path.join(os.path.dirname(_HERE), "include", "mathocr.h")
+    if not files or not os.path.exists(hdr):
+        return None
+    h = hashlib.sha256()
+    for f in files + [hdr]:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def exported_symbols():
-    return ["mocr_abi_version", "mocr_weight_count", "mocr_memory_tokens", "mocr_create", "mocr_destroy",
+    return ["mocr_abi_version", "mocr_source_hash", "mocr_device_count", "mocr_weight_count", "mocr_memory_tokens", "mocr_create", "mocr_destroy",
             "mocr_last_error", "mocr_load_weights", "mocr_set_images", "mocr_set_images_device", "mocr_encode",
             "mocr_get_memory", "mocr_decode", "mocr_decode_device", "mocr_decode_beam", "mocr_debug_encode_until",
             "mocr_set_timing", "mocr_get_timing", "mocr_set_encoder_pos", "mocr_set_cu_mask", "mocr_group_unique_id", "mocr_group_create",

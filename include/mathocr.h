@@ -109,6 +109,15 @@ typedef struct mocr_engine mocr_engine;
 
 int mocr_abi_version(void);
 
+/* sha256 (16 hex digits) of the sources the library was built from (the .hip and .h files of
+ * csrc sorted by name, then this header): the Python binding refuses a library whose sources
+ * changed. */
+const char* mocr_source_hash(void);
+
+/* HIP devices visible to the process (serving /health "device_available"); negative on a
+ * HIP error, message in mocr_last_error(NULL). */
+int mocr_device_count(void);
+
 /* Number of float32 values mocr_load_weights expects for this config.  The blob
  * is the concatenation, in order, of the tensors listed by
  * handwritten-math-ocr-api_amd/synth.py:param_specs (reference state_dict names,
