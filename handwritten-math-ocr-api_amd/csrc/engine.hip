@@ -1063,8 +1063,13 @@ struct mocr_engine {
   // stage 3 always (285 vs 301 us per block unfused at B=64, 384²); stage 4 only on request
   // (258 vs 211 us: a window's 64 padded rows re-read all of W_qkv, 1.8 GB from L2 per block,
   // and the padding costs 1.3x the GEMM's MFMA work)
-  bool noproj_fused(int C) const {
-    return attn_fused() && swin_attn_noproj_supported(C) && (C != 768 || (cfg.variant & MOCR_VARIANT_S4_FUSED_ATTN));
+  // stage 3 (C = 384) fused below 128 images: at B = 64 285 vs 301 us per block unfused,
+  // at B = 256 1054 vs 903 us (ln1 + qkv GEMM + window attention over the image tokens,
+  // tools/op_times.py --batch 256, profiles/r03/op_times_b256.log): the fused kernel
+  // re-streams W_qkv per window, the GEMM's efficiency grows with M
+  bool noproj_fused(int C, int B) const {
+    return attn_fused() && swin_attn_noproj_supported(C) &&
+           (C != 768 || (cfg.variant & MOCR_VARIANT_S4_FUSED_ATTN)) && (C != 384 || B < 128);
   }
   int attn_passes() const {
     return cfg.precision == MOCR_PRECISION_FP32 ? 0 : (cfg.precision == MOCR_PRECISION_BF16X3 ? 3 : 1);
@@ -1173,7 +1178,7 @@ struct mocr_engine {
           ap.wg = wg;
           timed(attn_n[s], 8.0 * rows * C * C + 4.0 * rows * kWinTok * C, 8.0 * rows * C + (dwl ? 4.0 : 2.0) * 4.0 * C * C,
                 [&] { launch_swin_attn_fused(ap, stream); });
-        } else if (b16 && noproj_fused(C)) {
+        } else if (b16 && noproj_fused(C, B)) {
           // norm1 + qkv + W-MSA in one kernel writing the ATT planes (wattn.hip), then proj
           SwinAttnParams ap{};
           ap.X = X;

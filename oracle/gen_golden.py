@@ -209,7 +209,7 @@ def make_res18_fixture(name, *, seed, variant, eos_boost, B, H, W, pos_seed, ste
 
 
 def make_batch_fixture(name, *, seed, variant, eos_boost, B, H, W, img_seed=1000, img_kind="uniform",
-                       steps, stop, n_logit_steps, stub, n_mem=2):
+                       steps, stop, n_logit_steps, stub, n_mem=2, n_logit_rows=None):
     pkg = _pkg()
     from oracle import model_ref
     w = apply_eos_boost(pkg.synth.make_weights(seed, variant), eos_boost)
@@ -237,7 +237,7 @@ def make_batch_fixture(name, *, seed, variant, eos_boost, B, H, W, img_seed=1000
                              img_kind=img_kind, steps=steps, stop=stop, glue_checked=glue is not None,
                              strings=strings)),
         ids=ys.numpy().astype(np.int32),
-        logits=logits[:n_mem, :n_logit_steps].astype(np.float32),
+        logits=logits[:(n_logit_rows or n_mem), :n_logit_steps].astype(np.float32),
         margins=margins,
         memory=mem[:n_mem].numpy().astype(np.float32),
         stage_sum=np.array([[float(s[i].double().sum()) for s in stages] for i in range(B)]),
@@ -297,12 +297,17 @@ def main(only=None):
                            W=320, img_kind="ink", pos_seed=6, steps=150, stub=stub)
     if only == "res18":
         return
+    if only == "bench_c2":
+        # config 2 only, teacher-forced logits of 8 rows x 8 steps (VERDICT r02 "Next" 4)
+        make_batch_fixture("g384_b64_bench", seed=1234, variant="init", eos_boost=0.0, B=64, H=384, W=384,
+                           steps=128, stop="batch", n_logit_steps=8, n_logit_rows=8, stub=stub)
+        return
     if only == "bench":
         # BASELINE configs at full size, on the bench's own inputs (bench.py: weights seed 1234 "init",
         # images PCG64 1000+i, 384x384): config 2 (Swin, B=64, greedy 128 steps), config 5
         # (ResNet18-trans, B=64, pos table seed 5), config 4 (beam 4, 256 steps: rows 0-1).
         make_batch_fixture("g384_b64_bench", seed=1234, variant="init", eos_boost=0.0, B=64, H=384, W=384,
-                           steps=128, stop="batch", n_logit_steps=4, stub=stub)
+                           steps=128, stop="batch", n_logit_steps=8, n_logit_rows=8, stub=stub)
         make_res18_fixture("r384_b64_bench", seed=1234, variant="init", eos_boost=0.0, B=64, H=384, W=384,
                            pos_seed=5, steps=128, stub=stub, n_logit_steps=4, n_logit_rows=2)
         make_beam_fixture("b384_k4_bench", seed=1234, variant="init", B=2, H=384, W=384, K=4, steps=256,

@@ -85,3 +85,50 @@ def crosscheck(weights: dict, images: np.ndarray):
     b, h, w, c = ours.shape
     theirs = hf_swin_from_weights(weights, images.shape[-2:])(x).last_hidden_state
     return float((ours.view(b, h * w, c) - theirs).abs().max()), float(theirs.abs().max())
+
+
+# ------------------------------------------------------------------ ResNet18 (BASELINE config 5)
+def hf_resnet18_from_weights(weights: dict):
+    """HF ``ResNetModel`` (``transformers/models/resnet/modeling_resnet.py``: BasicLayer,
+    shortcut conv1x1 + BN where the shape changes, no downsampling in stage 1) configured as
+    torchvision ``resnet18`` with a 1-channel stem, loaded with the same weights as
+    ``res18_ref``'s ``encoder.features.*`` (torchvision names)."""
+    from transformers import ResNetConfig, ResNetModel
+
+    cfg = ResNetConfig(num_channels=1, embedding_size=64, hidden_sizes=[64, 128, 256, 512], depths=[2, 2, 2, 2],
+                       layer_type="basic", hidden_act="relu", downsample_in_first_stage=False)
+    m = ResNetModel(cfg)
+    t = lambda k: torch.from_numpy(np.asarray(weights[k]))  # noqa: E731
+
+    def conv_bn(dst, conv, bn):
+        return {dst + "convolution.weight": t(conv + ".weight"), dst + "normalization.weight": t(bn + ".weight"),
+                dst + "normalization.bias": t(bn + ".bias"), dst + "normalization.running_mean": t(bn + ".running_mean"),
+                dst + "normalization.running_var": t(bn + ".running_var")}
+
+    f = "encoder.features."
+    sd = conv_bn("embedder.embedder.", f + "0", f + "1")  # features = conv1, bn1, relu, maxpool, layer1..4
+    for s in range(4):
+        for j in range(2):
+            src = f"{f}{4 + s}.{j}."
+            dst = f"encoder.stages.{s}.layers.{j}."
+            sd.update(conv_bn(dst + "layer.0.", src + "conv1", src + "bn1"))
+            sd.update(conv_bn(dst + "layer.1.", src + "conv2", src + "bn2"))
+            if src + "downsample.0.weight" in weights:
+                sd.update(conv_bn(dst + "shortcut.", src + "downsample.0", src + "downsample.1"))
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    assert not unexpected, unexpected
+    assert all(k.endswith("num_batches_tracked") for k in missing), missing
+    return m.eval()
+
+
+@torch.no_grad()
+def crosscheck_resnet18(weights: dict, images: np.ndarray):
+    """Return (max |Δ|, max |ref|) between ``res18_ref``'s backbone map [B, 512, h, w] (the
+    restated torchvision resnet18 without avgpool / fc, src/model_res18trans.py:16-32) and
+    HF's ``last_hidden_state``."""
+    from . import res18_ref
+    x = torch.from_numpy(images)
+    ours = res18_ref.build_model(weights).encoder.features(x)
+    theirs = hf_resnet18_from_weights(weights)(x).last_hidden_state
+    assert ours.shape == theirs.shape, (ours.shape, theirs.shape)
+    return float((ours - theirs).abs().max()), float(theirs.abs().max())

@@ -95,6 +95,16 @@ def test_shift_mask_regions(pH, pW, sh, sw):
     assert np.array_equal(a[:, None] == a[None, :], b[:, None] == b[None, :])
 
 
+
+def test_oracle_resnet18_matches_hf(pkg):
+    """oracle/res18_ref.py's torchvision-resnet18 restatement (BasicBlock, eval BN, 1-channel
+    stem) against HF transformers ResNetModel with the same weights (torchvision itself is
+    not installed): the two are independent implementations of the same network."""
+    from oracle import hf_crosscheck
+    w = pkg.synth.make_weights(1234, "init", arch="res18trans")
+    err, scale = hf_crosscheck.crosscheck_resnet18(w, pkg.synth.make_images(2, 384, 384, 77))
+    assert err < 1e-4 * max(1.0, scale), (err, scale)
+
 @pytest.mark.parametrize("name", ["r384_b8_pert", "r96x320_b4_eos"])
 def test_res18_oracle_reproduces_golden(pkg, golden, name):
     """ResNet18-trans (BASELINE config 5): the restatement reproduces the fixtures the

@@ -1,4 +1,4 @@
-"""Per-op HIP-event times of one 64-image 384x384 encode (the engine's timed() names),
+"""Per-op HIP-event times of one --batch-image (default 64) 384x384 encode (the engine's timed() names),
 fused vs unfused attention / MLP variants side by side.
 
     python tools/op_times.py [--encodes 3] [--filter s3.,s4.] [--lib LIB]
@@ -16,16 +16,17 @@ ap.add_argument("--encodes", type=int, default=3)
 ap.add_argument("--filter", default="")
 ap.add_argument("--variants", default="production,unfused_attn")
 ap.add_argument("--lib", default=None, help="libmathocr.so to load (an A/B build from tools/build_variant.sh)")
+ap.add_argument("--batch", type=int, default=64)
 a = ap.parse_args()
 pkg = importlib.import_module("handwritten-math-ocr-api_amd")
 if a.lib:
     pkg.engine.load_library(a.lib)
-imgs = pkg.synth.make_images(64, 384, 384)
+imgs = pkg.synth.make_images(a.batch, 384, 384)
 w = pkg.synth.make_weights(1234, "init")
 res = {}
 for vname in a.variants.split(","):
     var = () if vname == "production" else tuple(vname.split("+"))
-    eng = pkg.Engine(img_hw=(384, 384), max_batch=64, precision="bf16x3", variant=var)
+    eng = pkg.Engine(img_hw=(384, 384), max_batch=a.batch, precision="bf16x3", variant=var)
     eng.load_weights(w)
     eng.set_images(imgs)
     eng.encode()  # warm
