@@ -235,7 +235,7 @@ void check_config(const mocr_config& c) {
       "precision");
   req((c.variant & ~(MOCR_VARIANT_UNFUSED_ATTN | MOCR_VARIANT_UNFUSED_MLP | MOCR_VARIANT_DEC_UNFOLDED |
                       MOCR_VARIANT_S4_FUSED_ATTN | MOCR_VARIANT_WINDOW_ROWS | MOCR_VARIANT_DEC_NARROW |
-                      MOCR_VARIANT_LOGITS_F32)) == 0,
+                      MOCR_VARIANT_LOGITS_F32 | MOCR_VARIANT_S3_LARGE_BATCH)) == 0,
       "variant: unknown MOCR_VARIANT_* flag");
   req(c.sos_id >= 0 && c.sos_id < c.vocab && c.eos_id >= 0 && c.eos_id < c.vocab, "special ids");
 }
@@ -1069,8 +1069,13 @@ struct mocr_engine {
   // re-streams W_qkv per window, the GEMM's efficiency grows with M
   bool noproj_fused(int C, int B) const {
     return attn_fused() && swin_attn_noproj_supported(C) &&
-           (C != 768 || (cfg.variant & MOCR_VARIANT_S4_FUSED_ATTN)) && (C != 384 || B < 128);
+           (C != 768 || (cfg.variant & MOCR_VARIANT_S4_FUSED_ATTN)) && (C != 384 || !s3_large(B));
   }
+  // stage 3's kernels for >= 128 images: the unfused attention (above) and mlp.hip's fused
+  // C = 384 MLP, which runs 128 rows per workgroup on all 256 CUs (1152 workgroups at
+  // B = 256: 989 vs 1298 us per block for ln2 + fc1 + fc2; at B = 64 its 288 workgroups
+  // take two rounds, 476 vs 334 us, profiles/r03/mlp384_*.log)
+  bool s3_large(int B) const { return B >= 128 || (cfg.variant & MOCR_VARIANT_S3_LARGE_BATCH); }
   int attn_passes() const {
     return cfg.precision == MOCR_PRECISION_FP32 ? 0 : (cfg.precision == MOCR_PRECISION_BF16X3 ? 3 : 1);
   }
@@ -1226,7 +1231,7 @@ struct mocr_engine {
           gemm(proj_n[s], opATT, wop(w.projw), W(w.projb), X, nullptr, nullptr, (int)wrows, C, C, EPI_WINRES, &wg,
                rows);
         }
-        if (b16 && mlp_fused() && mlp_fused_supported(C)) {
+        if (b16 && mlp_fused() && mlp_fused_supported(C) && (C != 384 || s3_large(B))) {
           // norm2 + fc1 + GELU + fc2 + residual in one kernel (mlp.hip)
           MlpParams mp{};
           mp.X = X;

@@ -369,6 +369,318 @@ __global__ void __launch_bounds__(512) mlp_fused_kernel(MlpParams p) {
   }
 }
 
+// ---------------------------------------------------------------- stage 3 (C = 384)
+// The stage-1/2 kernel above keeps a whole W1 | W2 chunk double-buffered in LDS and
+// stages it through registers.  At C = 384 a 32-unit chunk is 96 KB (hi + lo), and the
+// LN'd rows (B fragments) plus the output accumulators of 128 rows take 384 registers
+// per lane of a 4-wave workgroup, so this kernel runs one wave per SIMD (512 registers:
+// 32 rows per wave) and fills its weight buffers by LDS-DMA (global_load_lds, no
+// staging VGPRs).  One W1 buffer and one W2 buffer (48 KB each) are refilled in
+// alternation: W2(jc) lands while GEMM 1 of chunk jc reads W1(jc), W1(jc + 1) lands
+// while GEMM 2 reads W2(jc); two raw barriers per chunk behind vmcnt(0) (each wave waits
+// for its own DMA, the barrier publishes it; __syncthreads would add a fence).
+//
+// GEMM 2's k order: the stage-1/2 kernel takes GEMM 2's B fragment p from hidden tiles
+// 2p, 2p+1 (lane group g: units 32p + 4g + r and 32p + 16 + 4g + r), which needs a
+// permuted W2 image that a 16-B DMA cannot build.  Here W1's rows are permuted instead:
+// LDS row u of chunk jc holds hidden unit jc*32 + pi(u), pi(16t + 4g + r) = 8g + 4t + r,
+// so lane group g's accumulators of the two hidden tiles are units 8g .. 8g + 7 in
+// order -- the B fragment over W2's natural k order.
+//
+// LDS images (per plane; the lo plane follows at +24 KB), both of 64-B rows:
+//  - W1: [12 k-steps][32 units] x 32 channels;
+//  - W2: [384 channels] x the chunk's 32 units;
+// the 16-B chunk c of row v stored at c ^ f((v >> 2) & 3), f = {0, 2, 3, 1} (the GEMM
+// ring kernel's swizzle: the fragment reads' lane groups hit 16 distinct 16-B slots),
+// applied on the DMA's per-lane source address (the LDS side of a DMA is lane-linear).
+// Every DMA source is a uniform base + one lane base + uniform offsets, and every
+// fragment read one lane base + an immediate.
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ int swz4(int r) { return (0x1320 >> (4 * ((r >> 2) & 3))) & 3; }  // {0,2,3,1}
+
+__device__ __forceinline__ uint32_t lds_u32(const char* p) {
+  return (uint32_t)reinterpret_cast<uintptr_t>((lds_ptr_t)(p));
+}
+// One 1-KB LDS-DMA piece: 16 B per lane from gbase + voff (uniform base, lane offset) to
+// LDS lds + 16 * lane.  Issued by inline asm so that hipcc does not see an LDS write in
+// flight: with __builtin_amdgcn_global_load_lds into a ring indexed at run time it puts a
+// vmcnt(0) before every fragment read.  The kernel waits for its own DMA (counted vmcnt
+// before each barrier); vector loads retire in order, so hipcc's own counts stay safe.
+// M0 is a reserved register (no clobber list entry): the asm saves and restores it.
+__device__ __forceinline__ void dma16(const char* gbase, uint32_t voff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(gbase), "s"(lds)
+      : "memory");
+}
+
+// timing probes (tools/build_variant.sh DIR -DMOCR_MLP384_PROBE=N; wrong results):
+// 1 no weight DMA, 2 no MFMA, 3 no vmcnt wait before the barriers, 4 every chunk's DMA
+// reads chunk 0 (an L2-resident 96 KB), 5 = 4 + 2
+#ifndef MOCR_MLP384_PROBE
+#define MOCR_MLP384_PROBE 0
+#endif
+template <int PASSES>
+__global__ void __launch_bounds__(256) mlp384_kernel(MlpParams p) {
+  constexpr int C = 384, HID = 4 * C, NC = 32, NCH = HID / NC, KS1 = C / 32, NCT = C / 16, TT = 2;
+  constexpr bool X3 = PASSES == 3;
+  constexpr int PL = X3 ? 2 : 1;
+  constexpr int PLB = NC * C * 2;             // bytes of one plane of a W1 or W2 chunk (24 KB)
+  constexpr int NPW = PL * (PLB / 1024) / 4;  // 1-KB DMA pieces per wave per matrix and chunk
+  static_assert(NPW * 4 * 1024 == PL * PLB && NPW <= KS1 && 2 * NPW <= NCT, "DMA split");
+  // a ring of three half-chunk slots (W1(0), W2(0), W1(1), ... in turn): two in flight
+  // while the MFMAs read the third
+  constexpr int SLOT = PL * PLB;
+  __shared__ __attribute__((aligned(16))) char ring[3 * SLOT];
+  __shared__ __attribute__((aligned(16))) float b1s[HID];
+  __shared__ __attribute__((aligned(16))) float b2s[C];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: piece offsets in SGPRs
+  const int j16 = lane & 15;
+  const int g = lane >> 4;
+  const long row0 = (long)blockIdx.x * 128 + wave * 16 * TT;
+  const char* w1g[2] = {static_cast<const char*>(p.w1), static_cast<const char*>(X3 ? p.w1lo : p.w1)};
+  const char* w2g[2] = {static_cast<const char*>(p.w2), static_cast<const char*>(X3 ? p.w2lo : p.w2)};
+
+  // W1 piece (plane q, k-step ks, half h): LDS rows u = 16 h + lane / 4 of block ks, slot
+  // lane % 4; row u is hidden unit pi(u) = 8 g + 4 h + (lane / 4) % 4 of the chunk, and
+  // slot s holds the channel chunk s ^ f(g) of k-step ks.
+  // W2 piece (plane q, pp): LDS rows r = 16 pp + lane / 4 (channels), slot s holds the
+  // chunk's hidden units 8 (s ^ f(g)) .. + 7.
+  const uint32_t lb1 = (uint32_t)((8 * g + ((lane >> 2) & 3)) * (C * 2) + (((lane & 3) ^ swz4(lane >> 2)) << 4));
+  const uint32_t lb2 = (uint32_t)((lane >> 2) * (HID * 2) + (((lane & 3) ^ swz4(lane >> 2)) << 4));
+  // (the empty asm makes the lane base look new in every call: hipcc would otherwise hoist
+  // the 24 per-piece 64-bit addresses out of the chunk loop and spill them)
+  // pieces [i0, i0 + n) of this wave's share (the chunk loop issues one piece per MFMA step:
+  // a burst of 12 DMA instructions stalls the wave's issue, and its MFMAs with it)
+  auto issue_w1 = [&](int jc, char* w1s, int i0, int n) {
+    if (MOCR_MLP384_PROBE == 1) return;
+    uint32_t lb = lb1;
+    asm volatile("" : "+v"(lb));
+#pragma unroll
+    for (int i = i0; i < i0 + n; ++i) {
+      // piece i of this wave: plane q = i / (NPW / PL) (compile-time), piece 4 (i % ..) + wave
+      const int q = i / (NPW / PL);
+      const int rem = (i - q * (NPW / PL)) * 4 + wave;
+      const int ks = rem >> 1, h = rem & 1;
+      const int jr = MOCR_MLP384_PROBE >= 4 ? 0 : jc;
+      const uint32_t off = (uint32_t)((jr * NC + 4 * h) * (C * 2) + ks * 64) + lb;
+      dma16(w1g[q], off, lds_u32(w1s) + q * PLB + rem * 1024);
+    }
+  };
+  auto issue_w2 = [&](int jc, char* w2s, int i0, int n) {
+    if (MOCR_MLP384_PROBE == 1) return;
+    uint32_t lb = lb2;
+    asm volatile("" : "+v"(lb));
+#pragma unroll
+    for (int i = i0; i < i0 + n; ++i) {
+      const int q = i / (NPW / PL);
+      const int pp = (i - q * (NPW / PL)) * 4 + wave;
+      const int jr = MOCR_MLP384_PROBE >= 4 ? 0 : jc;
+      const uint32_t off = (uint32_t)(pp * 16 * (HID * 2) + jr * NC * 2) + lb;
+      dma16(w2g[q], off, lds_u32(w2s) + q * PLB + pp * 1024);
+    }
+  };
+
+  // half-chunk hc: W1(hc / 2) if even, W2(hc / 2) if odd, into slot hc % 3
+  auto slot = [&](int hc) { return ring + (hc % 3) * SLOT; };
+  issue_w1(0, slot(0), 0, NPW);
+  issue_w2(0, slot(1), 0, NPW);
+  for (int i = tid; i < HID; i += 256) b1s[i] = p.b1[i];
+  for (int i = tid; i < C; i += 256) b2s[i] = p.b2[i];
+
+  // LayerNorm(norm2) of this wave's 2 x 16 rows into GEMM 1's B fragments (lane (g, j):
+  // row j of tile tt, channels 32 ks + 8 g .. + 7)
+  bf16x8 xb[TT][KS1][PL];
+#pragma unroll
+  for (int tt = 0; tt < TT; ++tt) {
+    const long row = min(row0 + tt * 16 + j16, p.M - 1);
+    const float* xr = p.X + (size_t)row * C + 8 * g;
+    float v[KS1][8];
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks) {
+      const floatx4 a = *reinterpret_cast<const floatx4*>(xr + 32 * ks);
+      const floatx4 b = *reinterpret_cast<const floatx4*>(xr + 32 * ks + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[ks][e] = a[e];
+        v[ks][4 + e] = b[e];
+      }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += v[ks][e];
+    s = xsum16_32(s);
+    const float mean = s / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = v[ks][e] - mean;
+        q += d * d;
+      }
+    q = xsum16_32(q);
+    const float rstd = 1.0f / sqrtf(q / (float)C + 1e-5f);
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks) {
+      const int ch = 32 * ks + 8 * g;
+      const floatx4 g0 = *reinterpret_cast<const floatx4*>(p.ln_g + ch);
+      const floatx4 g1 = *reinterpret_cast<const floatx4*>(p.ln_g + ch + 4);
+      const floatx4 c0 = *reinterpret_cast<const floatx4*>(p.ln_b + ch);
+      const floatx4 c1 = *reinterpret_cast<const floatx4*>(p.ln_b + ch + 4);
+      float y[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        y[e] = (v[ks][e] - mean) * rstd * g0[e] + c0[e];
+        y[4 + e] = (v[ks][4 + e] - mean) * rstd * g1[e] + c1[e];
+      }
+      bf16x8 hi, lo;
+      pack8(y, hi, lo);
+      xb[tt][ks][0] = hi;
+      if constexpr (X3) xb[tt][ks][PL - 1] = lo;
+    }
+  }
+
+  // fragment reads: row v = 16 t + j16 of a 64-B-row image, chunk g at g ^ f(j16 / 4)
+  const int fo = j16 * 64 + ((g ^ swz4(j16)) << 4);
+
+  floatx4 acc2[NCT][TT];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt) acc2[ct][tt] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  for (int jc = 0; jc < NCH; ++jc) {
+    // W1(jc) landed (this wave's pieces; W2(jc)'s may stay in flight), then visible to all;
+    // every wave is past GEMM 2 of chunk jc - 1, so its slot takes W1(jc + 1)
+    if (MOCR_MLP384_PROBE != 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
+    __builtin_amdgcn_s_barrier();
+    const bool nxt = jc + 1 < NCH;
+    char* s_w1n = slot(2 * jc + 2);
+    char* s_w2n = slot(2 * jc + 3);
+    const char* w1s = slot(2 * jc);
+    const char* w2s = slot(2 * jc + 1);
+    // GEMM 1: hidden^T [32 x 32] = W1[chunk, permuted rows] . LN(x)^T.  The fragments of
+    // k-step ks + 1 are read while the MFMAs of ks run; the scheduling barriers keep hipcc
+    // from hoisting every fragment read of the chunk to the top
+    floatx4 acc1[2][TT];
+#pragma unroll
+    for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+      for (int tt = 0; tt < TT; ++tt) acc1[ht][tt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 fa[2][2][PL];
+    auto rd1 = [&](int ks, bf16x8(&f)[2][PL]) {
+#pragma unroll
+      for (int ht = 0; ht < 2; ++ht) {
+        const int o = fo + ks * 2048 + ht * 1024;
+        f[ht][0] = *reinterpret_cast<const bf16x8*>(w1s + o);
+        if constexpr (X3) f[ht][PL - 1] = *reinterpret_cast<const bf16x8*>(w1s + PLB + o);
+      }
+    };
+    rd1(0, fa[0]);
+#pragma unroll
+    for (int ks = 0; ks < (MOCR_MLP384_PROBE == 2 || MOCR_MLP384_PROBE == 5 ? 0 : KS1); ++ks) {
+      if (ks + 1 < KS1) rd1(ks + 1, fa[(ks + 1) & 1]);
+      if (nxt && ks < NPW) issue_w1(jc + 1, s_w1n, ks, 1);
+#pragma unroll
+      for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+        for (int tt = 0; tt < TT; ++tt) {
+          const bf16x8 ah = fa[ks & 1][ht][0];
+          acc1[ht][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, xb[tt][ks][0], acc1[ht][tt], 0, 0, 0);
+          if constexpr (X3) {
+            const bf16x8 al = fa[ks & 1][ht][PL - 1];
+            acc1[ht][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, xb[tt][ks][1], acc1[ht][tt], 0, 0, 0);
+            acc1[ht][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, xb[tt][ks][0], acc1[ht][tt], 0, 0, 0);
+          }
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // W2(jc) landed and visible (W1(jc + 1)'s pieces may stay in flight); every wave is past
+    // GEMM 1, so its slot takes W2(jc + 1)
+    if (MOCR_MLP384_PROBE != 3) {
+      if (jc + 1 < NCH)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    // bias + GELU: lane group g holds hidden units jc*32 + 8 g .. + 7 of row j (tile ht,
+    // element r: unit 8 g + 4 ht + r), GEMM 2's B fragment
+    bf16x8 hb[TT][PL];
+    {
+      const floatx4 bb0 = *reinterpret_cast<const floatx4*>(b1s + jc * NC + 8 * g);
+      const floatx4 bb1 = *reinterpret_cast<const floatx4*>(b1s + jc * NC + 8 * g + 4);
+#pragma unroll
+      for (int tt = 0; tt < TT; ++tt) {
+        float h[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          h[r] = gelu_erf_fast(acc1[0][tt][r] + bb0[r]);
+          h[4 + r] = gelu_erf_fast(acc1[1][tt][r] + bb1[r]);
+        }
+        bf16x8 hi, lo;
+        pack8(h, hi, lo);
+        hb[tt][0] = hi;
+        if constexpr (X3) hb[tt][PL - 1] = lo;
+      }
+    }
+    // GEMM 2: out^T [384 x 32] += W2[:, chunk] . hidden^T, one channel tile per step, the
+    // next tile's fragments read ahead
+    bf16x8 fb[2][PL];
+    auto rd2 = [&](int ct, bf16x8(&f)[PL]) {
+      const int o = fo + ct * 1024;
+      f[0] = *reinterpret_cast<const bf16x8*>(w2s + o);
+      if constexpr (X3) f[PL - 1] = *reinterpret_cast<const bf16x8*>(w2s + PLB + o);
+    };
+    rd2(0, fb[0]);
+#pragma unroll
+    for (int ct = 0; ct < (MOCR_MLP384_PROBE == 2 || MOCR_MLP384_PROBE == 5 ? 0 : NCT); ++ct) {
+      if (ct + 1 < NCT) rd2(ct + 1, fb[(ct + 1) & 1]);
+      if (nxt && (ct & 1) == 0 && ct / 2 < NPW) issue_w2(jc + 1, s_w2n, ct / 2, 1);
+#pragma unroll
+      for (int tt = 0; tt < TT; ++tt) {
+        const bf16x8 ah = fb[ct & 1][0];
+        acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hb[tt][0], acc2[ct][tt], 0, 0, 0);
+        if constexpr (X3) {
+          const bf16x8 al = fb[ct & 1][PL - 1];
+          acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hb[tt][1], acc2[ct][tt], 0, 0, 0);
+          acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, hb[tt][0], acc2[ct][tt], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    }
+
+  // x += out + b2 (4 consecutive channels of one row per lane and tile); a row tile's 24
+  // loads are all issued before its first store (hipcc keeps a load behind an earlier
+  // store to the same buffer: one HBM round trip per tile otherwise)
+#pragma unroll
+  for (int tt = 0; tt < TT; ++tt) {
+    const long row = row0 + tt * 16 + j16;
+    if (row >= p.M) continue;
+    float* xr = p.X + (size_t)row * C + 4 * g;
+    floatx4 x[NCT];
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) x[ct] = *reinterpret_cast<const floatx4*>(xr + ct * 16);
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      const int ch = ct * 16 + 4 * g;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) x[ct][r] = x[ct][r] + (acc2[ct][tt][r] + b2s[ch + r]);
+      *reinterpret_cast<floatx4*>(xr + ct * 16) = x[ct];
+    }
+  }
+}
+
 template <int C, int TT, int NC>
 void launch_mlp_c(const MlpParams& p, hipStream_t s) {
   const unsigned grid = (unsigned)((p.M + 128 * TT - 1) / (128 * TT));
@@ -380,7 +692,7 @@ void launch_mlp_c(const MlpParams& p, hipStream_t s) {
 
 }  // namespace
 
-bool mlp_fused_supported(int C) { return C == 96 || C == 192; }
+bool mlp_fused_supported(int C) { return C == 96 || C == 192 || C == 384; }
 
 void launch_mlp_fused(const MlpParams& p, hipStream_t s) {
   if (p.M <= 0) return;
@@ -390,7 +702,15 @@ void launch_mlp_fused(const MlpParams& p, hipStream_t s) {
     // per s1 block; TT = 2 at C = 192 spills)
     case 96: launch_mlp_c<96, 2, 64>(p, s); break;
     case 192: launch_mlp_c<192, 1, 32>(p, s); break;
-    default: throw std::runtime_error("mlp: fused MLP built for C = 96, 192");
+    case 384: {
+      const unsigned grid = (unsigned)((p.M + 127) / 128);
+      if (p.w1lo)
+        mlp384_kernel<3><<<grid, 256, 0, s>>>(p);
+      else
+        mlp384_kernel<1><<<grid, 256, 0, s>>>(p);
+      break;
+    }
+    default: throw std::runtime_error("mlp: fused MLP built for C = 96, 192, 384");
   }
   MOCR_HIP_CHECK(hipGetLastError());
 }

@@ -68,7 +68,8 @@ enum {
   MOCR_VARIANT_DEFAULT = 0,
   MOCR_VARIANT_UNFUSED_ATTN = 1, /* Swin stages 1-2: LN-partition, qkv GEMM, window attention, proj */
                                  /* GEMM as separate kernels instead of wattn.hip's fused kernel     */
-  MOCR_VARIANT_UNFUSED_MLP = 2,  /* Swin stages 1-2: LN, fc1, fc2 instead of mlp.hip's fused kernel */
+  MOCR_VARIANT_UNFUSED_MLP = 2,  /* Swin stages 1-2 (and 3 at >= 128 images): LN, fc1, fc2 instead  */
+                                 /* of mlp.hip's fused kernels                                       */
   MOCR_VARIANT_DEC_UNFOLDED = 4, /* greedy decoder on the 8-kernel step (LayerNorms applied by their */
                                  /* consumers) instead of the folded 5-kernel step (decfold.hip)     */
   MOCR_VARIANT_S4_FUSED_ATTN = 8, /* Swin stage 4 (C = 768): norm1 + qkv + W-MSA in one kernel (two  */
@@ -79,8 +80,11 @@ enum {
                                   /* image's tokens in pixel order                                   */
   MOCR_VARIANT_DEC_NARROW = 32,   /* folded greedy step on decfold.hip's 16x16-tile fold GEMMs and    */
                                   /* decoder.hip's logits kernel instead of decwide.hip's wide tiles */
-  MOCR_VARIANT_LOGITS_F32 = 64    /* bf16x3 engines: the greedy step's fc_out on fp32-input MFMA     */
+  MOCR_VARIANT_LOGITS_F32 = 64,   /* bf16x3 engines: the greedy step's fc_out on fp32-input MFMA     */
                                   /* instead of bf16x3 (fc_out hi / lo planes)                        */
+  MOCR_VARIANT_S3_LARGE_BATCH = 128 /* Swin stage 3 takes its >= 128-image kernels at any batch      */
+                                    /* (unfused attention over the image tokens, mlp.hip's fused     */
+                                    /* C = 384 MLP), so small-batch parity tests cover that path     */
 };
 
 /* Greedy stopping rule (src/inference.py:23-25). */

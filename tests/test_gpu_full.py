@@ -92,6 +92,27 @@ def test_config2_swin_b64_greedy128(pkg, golden, precision):
     eng.close()
 
 
+def test_config2_as_benched_b256_chain(pkg, golden):
+    """Config 2 the way bench.py runs it: four 64-image batches encoded as one 256-image
+    batch (stage 3 on its >= 128-image kernels: unfused attention, mlp.hip's fused C = 384
+    MLP) and decoded as one 256-row chain.  The fixture's 64 images are rows 0-63 (the
+    others are the bench's next batches, seeds 1064+); their memory and ids must match the
+    fixture as at B = 64."""
+    g = golden("g384_b64_bench")
+    imgs = pkg.synth.make_images(256, 384, 384, seed0=1000)
+    eng = pkg.Engine(img_hw=(384, 384), max_batch=256, precision="bf16x3")
+    eng.load_weights(pkg.synth.make_weights(1234, "init"))
+    eng.encode(imgs)
+    mem = eng.memory()
+    assert rel_err(mem[:2], g["memory"]) < 1e-4
+    res = eng.decode(max_steps=128, stop="none")
+    rec = {"config": "C2 as benched (B=256 encode, 256-row chain)", "precision": "bf16x3"}
+    n_full = check_ids(res.ids[:64], g["ids"], g["margins"], tie=1e-4, record=rec)
+    assert n_full >= 60, n_full
+    assert rec["rows_equal_all_columns"] >= C2_ROWS_EQUAL_FLOOR["bf16x3"], rec
+    eng.close()
+
+
 def test_config5_res18trans_b64_greedy128(pkg, golden):
     g = golden("r384_b64_bench")
     m = g["meta"]

@@ -51,12 +51,14 @@ def test_encoder_stages_match_oracle(pkg, g384):
 
 
 @pytest.mark.parametrize("variant", [(), ("unfused_attn",), ("unfused_attn", "unfused_mlp"), ("s4_fused_attn",),
-                                     ("window_rows",), ("unfused_attn", "window_rows")])
+                                     ("window_rows",), ("unfused_attn", "window_rows"), ("s3_large_batch",),
+                                     ("s3_large_batch", "unfused_mlp")])
 def test_bf16x3_encoder_stages_match_oracle(pkg, golden, variant):
     """bf16x3 encoder stage by stage: the fused stage-1/2 attention half (wattn.hip) and
     MLP half (mlp.hip), the stage-3 no-proj kernel, the stage-4 two-half kernel (off in
-    production), and the unfused kernels they replace (MOCR_VARIANT_* flags), all within
-    1e-4 of the fp32 oracle.  384x384: the stage-1 map is 96x96, padded to 98
+    production), stage 3's >= 128-image path (unfused attention, mlp.hip's C = 384 fused
+    MLP) and the unfused kernels they replace (MOCR_VARIANT_* flags), all within 1e-4 of
+    the fp32 oracle.  384x384: the stage-1 map is 96x96, padded to 98
     (zero tokens) and rolled by 3 on odd blocks."""
     g = golden("g384_b2_pert")
     m = g["meta"]
@@ -255,13 +257,14 @@ def test_wide_chain_rows_bitwise(pkg, g384, precision):
     np.testing.assert_array_equal(out[100].logits[:2], out[2].logits)
 
 
-@pytest.mark.parametrize("precision,tol", [("bf16x3", 1e-4), ("bf16", 3e-2)])
-def test_bf16_encoder_modes(pkg, golden, precision, tol):
+@pytest.mark.parametrize("precision,tol,variant", [("bf16x3", 1e-4, ()), ("bf16", 3e-2, ()),
+                                                   ("bf16", 3e-2, ("s3_large_batch",))])
+def test_bf16_encoder_modes(pkg, golden, precision, tol, variant):
     """bf16 MFMA encoder GEMMs: bf16x3 (split hi/lo operands) keeps fp32-level memory
     error and the golden token ids; plain bf16 is checked for its looser error only."""
     g = golden("g384_b2_pert")
     m = g["meta"]
-    eng, _ = make_engine(pkg, m, precision=precision)
+    eng, _ = make_engine(pkg, m, precision=precision, variant=variant)
     eng.encode(pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m["img_kind"]))
     assert rel_err(eng.memory(), g["memory"]) < tol
     res = eng.decode(max_steps=m["steps"], stop="none", forced=g["ids"], want_logits=True)
