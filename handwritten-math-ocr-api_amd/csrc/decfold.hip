@@ -280,7 +280,8 @@ __global__ void __launch_bounds__(64 * NW) foldgemm_kernel(FoldGemmParams p) {
 // t-1 for its row (select.h; the head-0 workgroup does the bookkeeping), then takes q|k|v
 // of the selected token from the tables and writes its 32 columns of x = emb + pos --
 // the work of a separate argmax kernel at the end of step t-1, without its launch.
-template <bool SELF, bool ZS, bool SEL, int NIT>
+// F24: K/V (and the self-attention cache) in fp24 planes (common.h).
+template <bool SELF, bool ZS, bool SEL, int NIT, bool F24>
 __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   constexpr int LPR = 8;  // lanes per key row
   constexpr int RPW = 8;  // key rows per wave instruction
@@ -300,15 +301,20 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   const int n_cached = SELF ? t : n;
   const int m_first = wave * RPW + rsub;
 
-  const float* Kb = p.K + (size_t)b * p.kv_b_stride + cc;
-  const float* Vb = p.V + (size_t)b * p.kv_b_stride + cc;
+  const size_t kvb = F24 ? (size_t)b * p.f24_b + (size_t)h * p.f24_h + li * 4 : (size_t)b * p.kv_b_stride + cc;
+  const size_t kvr = F24 ? 32 : (size_t)p.kv_row_stride;
   floatx4 kk[NIT], vv[NIT];
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int m = m_first + it * 4 * RPW;
-    const size_t ml = (size_t)(m < n_cached ? m : 0);  // row 0 is allocated; masked below
-    kk[it] = ld_stream4(Kb + ml * p.kv_row_stride);
-    vv[it] = ld_stream4(Vb + ml * p.kv_row_stride);
+    const size_t o = kvb + (size_t)(m < n_cached ? m : 0) * kvr;  // row 0 is allocated; masked below
+    if constexpr (F24) {
+      kk[it] = ld_stream_fp24x4(p.K16 + o, p.K8 + o);
+      vv[it] = ld_stream_fp24x4(p.V16 + o, p.V8 + o);
+    } else {
+      kk[it] = ld_stream4(p.K + o);
+      vv[it] = ld_stream4(p.V + o);
+    }
   }
   constexpr int NP = SELF ? 3 : 1;  // q (| k | v)
   floatx4 zv[NP], sv[NP], cv[NP];
@@ -350,6 +356,13 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   }
   const floatx4 q4 = zv[0];
   const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (SELF && F24) {  // the newest key / value as every later step reads them from the cache
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      zv[1][e] = fp24_round(zv[1][e]);
+      zv[2][e] = fp24_round(zv[2][e]);
+    }
+  }
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int m = m_first + it * 4 * RPW;
@@ -362,9 +375,15 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   }
   if constexpr (SELF) {
     if (wave == 0 && rsub == 0 && !dec_skip(p.st, t)) {
-      const size_t o = (size_t)b * p.kv_b_stride + (size_t)t * p.kv_row_stride + cc;
-      *reinterpret_cast<floatx4*>(p.kcache + o) = zv[1];
-      *reinterpret_cast<floatx4*>(p.vcache + o) = zv[2];
+      if constexpr (F24) {
+        const size_t o = kvb + (size_t)t * 32;
+        st_fp24x4(p.kc16 + o, p.kc8 + o, zv[1]);
+        st_fp24x4(p.vc16 + o, p.vc8 + o, zv[2]);
+      } else {
+        const size_t o = kvb + (size_t)t * p.kv_row_stride;
+        *reinterpret_cast<floatx4*>(p.kcache + o) = zv[1];
+        *reinterpret_cast<floatx4*>(p.vcache + o) = zv[2];
+      }
     }
   }
 
@@ -487,27 +506,37 @@ void launch_dec_foldattn(const FoldAttnParams& p, bool self_attn, hipStream_t s)
   if (p.sel_on && (!self_attn || zs || !p.qtab || !p.qpos || !p.emb || !p.pos || !p.x || p.sel.t != p.t - 1 ||
                    (p.sel.part && p.sel.nparts > 512)))
     throw std::runtime_error("foldattn: the selection runs in layer 0's self-attention of step sel.t + 1");
+  const bool f24 = p.K16 != nullptr;
+  if (f24 && (!p.K8 || !p.V16 || !p.V8 || (self_attn && (!p.kc16 || !p.kc8 || !p.vc16 || !p.vc8))))
+    throw std::runtime_error("foldattn: fp24 K/V needs both planes of K and V (and of the cache)");
   if (p.B <= 0) return;
   const int nit = (p.n + 31) / 32;  // 32 key rows per workgroup pass (4 waves x 8 rows)
   const dim3 grid(p.B, kD / 32);
-#define MOCR_FA(N)                                                                    \
-  case N:                                                                             \
-    if (self_attn && zs)                                                              \
-      dec_foldattn_kernel<true, true, false, N><<<grid, 256, 0, s>>>(p);              \
-    else if (self_attn && p.sel_on)                                                   \
-      dec_foldattn_kernel<true, false, true, N><<<grid, 256, 0, s>>>(p);              \
-    else if (self_attn)                                                               \
-      dec_foldattn_kernel<true, false, false, N><<<grid, 256, 0, s>>>(p);             \
-    else if (zs)                                                                      \
-      dec_foldattn_kernel<false, true, false, N><<<grid, 256, 0, s>>>(p);             \
-    else                                                                              \
-      dec_foldattn_kernel<false, false, false, N><<<grid, 256, 0, s>>>(p);            \
+#define MOCR_FA2(N, F)                                                     \
+  if (self_attn && zs)                                                     \
+    dec_foldattn_kernel<true, true, false, N, F><<<grid, 256, 0, s>>>(p);  \
+  else if (self_attn && p.sel_on)                                          \
+    dec_foldattn_kernel<true, false, true, N, F><<<grid, 256, 0, s>>>(p);  \
+  else if (self_attn)                                                      \
+    dec_foldattn_kernel<true, false, false, N, F><<<grid, 256, 0, s>>>(p); \
+  else if (zs)                                                             \
+    dec_foldattn_kernel<false, true, false, N, F><<<grid, 256, 0, s>>>(p); \
+  else                                                                     \
+    dec_foldattn_kernel<false, false, false, N, F><<<grid, 256, 0, s>>>(p);
+#define MOCR_FA(N)          \
+  case N:                   \
+    if (f24) {              \
+      MOCR_FA2(N, true)     \
+    } else {                \
+      MOCR_FA2(N, false)    \
+    }                       \
     break;
   switch (nit) {
     MOCR_FA(1) MOCR_FA(2) MOCR_FA(3) MOCR_FA(4) MOCR_FA(5) MOCR_FA(6) MOCR_FA(7) MOCR_FA(8) MOCR_FA(9)
     default: throw std::runtime_error("foldattn: at most 288 keys");
   }
 #undef MOCR_FA
+#undef MOCR_FA2
   MOCR_HIP_CHECK(hipGetLastError());
 }
 

@@ -235,7 +235,7 @@ void check_config(const mocr_config& c) {
       "precision");
   req((c.variant & ~(MOCR_VARIANT_UNFUSED_ATTN | MOCR_VARIANT_UNFUSED_MLP | MOCR_VARIANT_DEC_UNFOLDED |
                       MOCR_VARIANT_S4_FUSED_ATTN | MOCR_VARIANT_WINDOW_ROWS | MOCR_VARIANT_DEC_NARROW |
-                      MOCR_VARIANT_LOGITS_F32 | MOCR_VARIANT_S3_LARGE_BATCH)) == 0,
+                      MOCR_VARIANT_LOGITS_F32 | MOCR_VARIANT_S3_LARGE_BATCH | MOCR_VARIANT_KV_F32)) == 0,
       "variant: unknown MOCR_VARIANT_* flag");
   req(c.sos_id >= 0 && c.sos_id < c.vocab && c.eos_id >= 0 && c.eos_id < c.vocab, "special ids");
 }
@@ -315,6 +315,10 @@ struct mocr_engine {
   float *ds_sa = nullptr, *ds_ca = nullptr, *ds_ff = nullptr;  // row-stat partials [B][16][2]
   float* dlogits_hist = nullptr;
   float *kcache = nullptr, *vcache = nullptr;
+  // fp24 planes (common.h) of the cross-attention K/V and of the self-attention cache that
+  // the folded greedy step streams in bf16x3 engines (kv24())
+  uint16_t *MEMKV16 = nullptr, *kc16 = nullptr, *vc16 = nullptr;
+  uint8_t *MEMKV8 = nullptr, *kc8 = nullptr, *vc8 = nullptr;
   int32_t *ids = nullptr, *feed = nullptr, *forced = nullptr, *finished = nullptr;
   float* logp = nullptr;
   DecodeState* st = nullptr;
@@ -375,7 +379,7 @@ struct mocr_engine {
                     ds_sa,   ds_ca,   ds_ff,
                     dlogits_hist, kcache, vcache, ids, feed, forced, finished, logp, st, XWh, XWl, ATTh, ATTl,
                     HIDh, HIDl, MEMh, MEMl, dwh, dwl, kvwh, kvwl, bscore, bfin, bseq[0], bseq[1],
-                    bslot[0], bslot[1], fold_buf, qtab, qpos, dzqkv, dpart};
+                    bslot[0], bslot[1], fold_buf, qtab, qpos, dzqkv, dpart, MEMKV16, MEMKV8, kc16, kc8, vc16, vc8};
     for (void* p : bufs)
       if (p) (void)hipFree(p);
     for (void* p : frag_allocs)
@@ -656,6 +660,7 @@ struct mocr_engine {
       timed("crosskv", 2.0 * rows * 512 * 256, 4.0 * (rows * 256.0 + 512 * 256 + rows * 512.0),
             [&] { launch_rowgemm(q, stream); });
     }
+    split_memkv24(B);
   }
 
   // ---------------------------------------------------------------- setup
@@ -755,6 +760,15 @@ struct mocr_engine {
     dpart = dalloc<float>(B * Vpad / 4);
     kcache = dalloc<float>(L * R * cfg.max_pos * d);
     vcache = dalloc<float>(L * R * cfg.max_pos * d);
+    if (kv24()) {
+      const size_t nkv = (size_t)B * M * L * 2 * d, nc = L * R * cfg.max_pos * d;
+      MEMKV16 = dalloc<uint16_t>(nkv);
+      MEMKV8 = dalloc<uint8_t>(nkv);
+      kc16 = dalloc<uint16_t>(nc);
+      kc8 = dalloc<uint8_t>(nc);
+      vc16 = dalloc<uint16_t>(nc);
+      vc8 = dalloc<uint8_t>(nc);
+    }
     ld_ids = cfg.max_pos + 1;
     if (cfg.max_beam > 0) {
       bscore = dalloc<float>(R);
@@ -1044,6 +1058,21 @@ struct mocr_engine {
   bool fold_greedy() const { return !(cfg.variant & MOCR_VARIANT_DEC_UNFOLDED); }
   // wide-tile fold GEMMs and logits (decwide.hip) unless MOCR_VARIANT_DEC_NARROW
   bool fold_wide() const { return fold_greedy() && !(cfg.variant & MOCR_VARIANT_DEC_NARROW); }
+  // the folded greedy step of bf16x3 engines streams its K/V as fp24 (common.h) unless
+  // MOCR_VARIANT_KV_F32; fp32 engines keep fp32 K/V
+  bool kv24() const {
+    return fold_greedy() && cfg.precision == MOCR_PRECISION_BF16X3 && !(cfg.variant & MOCR_VARIANT_KV_F32);
+  }
+  // the fp24 planes of the cross-attention K/V of the B encoded images
+  void split_memkv24(int B) {
+    if (!kv24()) return;
+    const int d = cfg.d_model;
+    const size_t kv_layer = (size_t)cfg.max_batch * M * 2 * d;
+    timed("memkv(fp24)", 0, 7.0 * cfg.n_layers * (double)B * M * 2 * d, [&] {
+      for (int l = 0; l < cfg.n_layers; ++l)
+        launch_split_kv_fp24(MEMKV + l * kv_layer, MEMKV16 + l * kv_layer, MEMKV8 + l * kv_layer, B, M, stream);
+    });
+  }
   // the wide logits on bf16x3 MFMA (fc_out planes) in bf16x3 engines unless MOCR_VARIANT_LOGITS_F32
   bool logits_x3() const {
     return fold_wide() && cfg.precision == MOCR_PRECISION_BF16X3 && !(cfg.variant & MOCR_VARIANT_LOGITS_F32);
@@ -1278,6 +1307,7 @@ struct mocr_engine {
          (long)B * M);
     gemm("crosskv", Operand{MEM, MEMh, MEMl}, Operand{kvw_all, kvwh, kvwl}, kvb_all, MEMKV, nullptr, nullptr, B * M,
          (int)(L * 2 * d), (int)d, EPI_STORE, nullptr, (long)B * M, (int)(2 * d), (size_t)cfg.max_batch * M * 2 * d);
+    split_memkv24(B);
     MOCR_HIP_CHECK(hipStreamSynchronize(stream));
     if (timing) flush_timing();
     encoded = true;
@@ -1433,6 +1463,11 @@ struct mocr_engine {
         a.x = dx;
       }
       a.K = kc; a.V = vc; a.kcache = kc; a.vcache = vc;
+      if (kv24()) {  // head-major [rows][8][max_pos][32] per layer
+        const size_t o = l * cache_layer;
+        a.K16 = a.kc16 = kc16 + o; a.K8 = a.kc8 = kc8 + o; a.V16 = a.vc16 = vc16 + o; a.V8 = a.vc8 = vc8 + o;
+        a.f24_b = (size_t)8 * cfg.max_pos * 32; a.f24_h = (size_t)cfg.max_pos * 32;
+      }
       a.kv_b_stride = (size_t)cfg.max_pos * d; a.kv_row_stride = d; a.n = t + 1;
       launch_dec_foldattn(a, true, s);
       FoldGemmParams g{};
@@ -1448,6 +1483,11 @@ struct mocr_engine {
       a = FoldAttnParams{};
       a.st = stp; a.t = t; a.B = B; a.out = datt; a.z = dq; a.z_ld = d; a.z_stats = ds_sa; a.s = f.sq; a.c = f.cq;
       a.K = memk; a.V = memk + d; a.kv_b_stride = (size_t)M * 2 * d; a.kv_row_stride = 2 * d; a.n = M;
+      if (kv24()) {  // head-major [B][k | v][8][M][32] per layer
+        const size_t o = l * kv_layer, ov = o + (size_t)8 * M * 32;
+        a.K16 = MEMKV16 + o; a.K8 = MEMKV8 + o; a.V16 = MEMKV16 + ov; a.V8 = MEMKV8 + ov;
+        a.f24_b = (size_t)2 * 8 * M * 32; a.f24_h = (size_t)M * 32;
+      }
       launch_dec_foldattn(a, false, s);
       g = FoldGemmParams{};
       g.B = B; g.t = t; g.st = stp;

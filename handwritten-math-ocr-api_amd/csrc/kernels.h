@@ -138,6 +138,10 @@ void launch_swin_attn_noproj(const SwinAttnParams& p, hipStream_t s);
 
 // x -> bf16 hi (and lo) planes.
 void launch_split_bf16(const float* x, uint16_t* hi, uint16_t* lo, size_t n, hipStream_t s);
+// Cross-attention K/V [rows = B * M][2 * 256] fp32 -> fp24 planes (common.h fp24_*: 16-bit
+// plane of bits 31..16, 8-bit plane of bits 15..8 after rounding at bit 8), head-major
+// [B][k | v][8 heads][M][32] (FoldAttnParams f24_*)
+void launch_split_kv_fp24(const float* kv, uint16_t* hi, uint8_t* mid, int B, int M, hipStream_t s);
 
 // ------------------------------------------------------------------ decoder
 // Every decode kernel takes its step index t as an argument (one captured graph per
@@ -256,6 +260,14 @@ struct FoldAttnParams {
   const float* K;
   const float* V;
   float *kcache, *vcache;  // self only: this layer's cache (same strides as K/V)
+  // fp24 K/V (common.h): the planes replace K / V / kcache / vcache when K16 is set.  Head-
+  // major: key m of head h of row b at b * f24_b + h * f24_h + 32 m (a head's 32 columns
+  // of consecutive keys are adjacent, so the 16- and 8-bit loads fill whole lines)
+  const uint16_t *K16, *V16;
+  const uint8_t *K8, *V8;
+  uint16_t *kc16, *vc16;
+  uint8_t *kc8, *vc8;
+  size_t f24_b, f24_h;
   size_t kv_b_stride;
   int kv_row_stride;
   int n;                   // keys (self: t + 1)

@@ -82,9 +82,11 @@ enum {
                                   /* decoder.hip's logits kernel instead of decwide.hip's wide tiles */
   MOCR_VARIANT_LOGITS_F32 = 64,   /* bf16x3 engines: the greedy step's fc_out on fp32-input MFMA     */
                                   /* instead of bf16x3 (fc_out hi / lo planes)                        */
-  MOCR_VARIANT_S3_LARGE_BATCH = 128 /* Swin stage 3 takes its >= 128-image kernels at any batch      */
-                                    /* (unfused attention over the image tokens, mlp.hip's fused     */
-                                    /* C = 384 MLP), so small-batch parity tests cover that path     */
+  MOCR_VARIANT_S3_LARGE_BATCH = 128, /* Swin stage 3 takes its >= 128-image kernels at any batch     */
+                                     /* (unfused attention over the image tokens, mlp.hip's fused    */
+                                     /* C = 384 MLP), so small-batch parity tests cover that path    */
+  MOCR_VARIANT_KV_F32 = 256          /* bf16x3 engines: the greedy step streams fp32 K/V instead of  */
+                                     /* fp24 (16 + 8-bit planes, relative rounding <= 2^-16)         */
 };
 
 /* Greedy stopping rule (src/inference.py:23-25). */

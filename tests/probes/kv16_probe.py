@@ -22,9 +22,18 @@ _orig = F._in_projection_packed
 MODE = {"dt": None}
 
 
+def fp24(x):
+    """fp32 rounded to its top 24 bits (sign, exponent, 15 mantissa bits): round to nearest
+    at bit 8, the storage a 16-bit + 8-bit plane pair holds."""
+    bits = x.contiguous().view(torch.int32)
+    return ((bits + 0x80) & ~0xFF).view(torch.float32)
+
+
 def patched(q, k, v, w, b=None):
     qq, kk, vv = _orig(q, k, v, w, b)
-    if MODE["dt"] is not None:
+    if MODE["dt"] == "fp24":
+        kk, vv = fp24(kk), fp24(vv)
+    elif MODE["dt"] is not None:
         kk = kk.to(MODE["dt"]).float()
         vv = vv.to(MODE["dt"]).float()
     return qq, kk, vv
@@ -47,12 +56,12 @@ for name in names:
     MODE["dt"] = None
     ref = model_ref.teacher_forced_logits(model, mem, ys)
     marg = model_ref.top2_margins(ref)
-    for dt in (torch.float16, torch.bfloat16):
+    for dt in ("fp24", torch.float16, torch.bfloat16):
         MODE["dt"] = dt
         out = model_ref.teacher_forced_logits(model, mem, ys)
         d = (out - ref).abs().max().item()
         flips = (out.argmax(-1) != ref.argmax(-1)).numpy()
         fm = marg[flips] if flips.any() else np.array([])
-        print(f"{name}: K/V {str(dt)[6:]}: max|d logits| {d:.2e}, argmax flips {int(flips.sum())} of {flips.size} "
+        print(f"{name}: K/V {str(dt).replace('torch.', '')}: max|d logits| {d:.2e}, argmax flips {int(flips.sum())} of {flips.size} "
               f"(their fp32 top-2 margins: {np.round(fm, 6).tolist()[:6]}), "
               f"steps with margin < 1e-4: {int((marg < 1e-4).sum())}", flush=True)

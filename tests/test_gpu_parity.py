@@ -120,12 +120,12 @@ def test_teacher_forced_logits_384(pkg, g384):
     np.testing.assert_array_equal(res.ids[:, 1:], g["ids"][:, 1:])
 
 
-@pytest.mark.parametrize("variant", [(), ("logits_f32",)])
+@pytest.mark.parametrize("variant", [(), ("logits_f32",), ("kv_f32",)])
 @pytest.mark.parametrize("name", ["g384_b2_pert", "g96x320_b4_eos"])
 def test_teacher_forced_logits_bf16x3(pkg, golden, name, variant):
     """The bench precision (bf16x3 encoder GEMMs, attention, fold GEMMs and logits of the
-    decode step; MOCR_VARIANT_LOGITS_F32: fp32 logits): teacher-forced logits within the
-    north star's 1e-3, ids token-exact."""
+    decode step, fp24 K/V; MOCR_VARIANT_LOGITS_F32: fp32 logits; MOCR_VARIANT_KV_F32: fp32
+    K/V): teacher-forced logits within the north star's 1e-3, ids token-exact."""
     g = golden(name)
     m = g["meta"]
     eng, _ = make_engine(pkg, m, precision="bf16x3", variant=variant)
