@@ -25,14 +25,12 @@ cut -c1-400 $O/bench.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_bench -o run -- \
   python3 bench.py --steps 6 --warmup 2 --no-cpu-baseline > $O/prof_bench.log 2>&1 \
   || { echo "ROCPROF FAILED"; tail -20 $O/prof_bench.log; exit 1; }
-python3 tools/trace_phase_stats.py $O/prof_bench/run_kernel_trace.csv "gemm_x3_stagq_kernel<1, 9, 4, 3, 2>" 6 \
-  --json $O/trace_iso_s3fc1.json > /dev/null || echo "trace phase stats failed"
-python3 tools/trace_phase_stats.py $O/prof_bench/run_kernel_trace.csv "swin_attn_noproj_kernel<384, 3, 3, 12, 2>" 6 \
-  --json $O/trace_iso_s3attn.json > /dev/null || echo "trace phase stats failed"
+python3 tools/trace_phase_stats.py $O/prof_bench/run_kernel_trace.csv "mlp384_kernel<3>" 6 \
+  --json $O/trace_iso_s3mlp.json > /dev/null || echo "trace phase stats failed"
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o run -- \
-  python3 tools/profile_encoder.py --decode-steps 8 > $O/pmc_f.log 2>&1 || { echo "PMC F FAILED"; exit 1; }
+  python3 tools/profile_encoder.py --batch 256 --decode-steps 8 > $O/pmc_f.log 2>&1 || { echo "PMC F FAILED"; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o run -- \
-  python3 tools/profile_encoder.py --decode-steps 8 > $O/pmc_w.log 2>&1 || { echo "PMC W FAILED"; exit 1; }
+  python3 tools/profile_encoder.py --batch 256 --decode-steps 8 > $O/pmc_w.log 2>&1 || { echo "PMC W FAILED"; exit 1; }
 python3 tools/pmc_traffic.py $O/pmc_f/run_counter_collection.csv $O/pmc_w/run_counter_collection.csv \
   $O/pmc_traffic_bf16x3.json 8 || echo "pmc_traffic mapping failed"
 echo done

@@ -32,12 +32,18 @@ def classes_in_order(mlp_fused=(), attn_fused=(), attn_noproj=()):
             elif s + 1 in attn_noproj:
                 names += [f"s{s+1}.attn", f"s{s+1}.proj"]
             else:
-                names += [f"s{s+1}.ln_partition", f"s{s+1}.qkv", f"s{s+1}.wattn", f"s{s+1}.proj"]
-            names += [f"s{s+1}.mlp"] if s + 1 in mlp_fused else [f"s{s+1}.layernorm", f"s{s+1}.fc1", f"s{s+1}.fc2"]
+                names += [f"s{s+1}.ln1", f"s{s+1}.qkv", f"s{s+1}.wattn", f"s{s+1}.proj"]
+            names += [f"s{s+1}.mlp"] if s + 1 in mlp_fused else [f"s{s+1}.ln2", f"s{s+1}.fc1", f"s{s+1}.fc2"]
         if s < 3:
             names += [f"merge{s+1}.ln", f"merge{s+1}"]
     names += ["split(memory)", "memproj", "crosskv"]
     return names
+
+
+def with_memkv24(names, kn):
+    """bf16x3 engines append the fp24 split of the cross K/V (one dispatch per layer)."""
+    n = sum("split_kv_fp24" in k for k in kn)
+    return names + ["memkv(fp24)"] * n
 
 
 def main(fetch_csv, write_csv, out, decode_steps=0):
@@ -48,10 +54,11 @@ def main(fetch_csv, write_csv, out, decode_steps=0):
     w = [r for r in csv.DictReader(open(write_csv)) if keep(r)]
     assert len(f) == len(w)
     kn = [r["Kernel_Name"] for r in f]
-    fused = sorted({1 if "mlp_fused_kernel<96" in k else 2 for k in kn if "mlp_fused" in k})
+    fused = sorted({1 if "mlp_fused_kernel<96" in k else 2 for k in kn if "mlp_fused" in k} |
+                   ({3} if any("mlp384_kernel" in k for k in kn) else set()))
     afused = sorted({1 if "swin_attn_kernel<96" in k else 2 for k in kn if "swin_attn_kernel" in k})
     anoproj = [3] if any("swin_attn_noproj_kernel" in k for k in kn) else []
-    names = classes_in_order(fused, afused, anoproj)
+    names = with_memkv24(classes_in_order(fused, afused, anoproj), kn)
     # load-time bf16 splits before the stem: weights, kv-weights, and (bf16x3) the folded
     # decoder weights; fp32 mode has none
     n_split = next(i for i, k in enumerate(kn) if "stem" in k)
