@@ -184,7 +184,8 @@ def survey_decode_step_bytes(rows, t, L=8, d=256, ff=512, V=5075, M=144):
 def roofline_decode(stats, precision, rows, steps):
     """The greedy decode step (41 graph-captured dependent kernels) against HBM: SURVEY
     §8(d)'s algorithmic bytes of a step (bf16 K/V and weights) / the HIP-event step time,
-    with the engine's fp32-as-built bytes (engine.hip decode_step_bytes) beside them."""
+    with the engine's as-built bytes (engine.hip decode_step_bytes: fp32 weights or their
+    bf16x3 planes, fp24 K/V in bf16x3 engines) beside them."""
     d = stats.get("decode.greedy")
     if not d or not d["launches"]:
         return None

@@ -1733,16 +1733,18 @@ struct mocr_engine {
     return n;
   }
 
-  // Algorithmic work of greedy step t over B rows (SURVEY.md §8(d), fp32 as built): every
-  // decoder weight and fc_out once, the cross-attention K/V of all layers, the self-attention
-  // K/V of positions 0..t read and position t written, the logits written.  FLOP: the
-  // per-row projections 2*(6 d^2 + 2 d ff) per layer + 2 V d, attention 4 d (keys) per layer.
+  // Algorithmic work of greedy step t over B rows (as built: fp32, or
+  // bf16x3 weight planes (4 B per weight) and fp24 K/V (3 B) under kv24()): every decoder
+  // weight and fc_out once, the cross-attention K/V of all layers, the self-attention K/V
+  // of positions 0..t read and position t written, the logits written.  FLOP: the per-row
+  // projections 2*(6 d^2 + 2 d ff) per layer + 2 V d, attention 4 d (keys) per layer.
   double decode_step_bytes(int B, int t) const {
     const double d = cfg.d_model, ff = cfg.d_ff, L = cfg.n_layers, V = cfg.vocab;
     const double weights = L * (6 * d * d + 2 * d * ff) + V * d;
     const double cross = (double)B * M * 2 * d * L;
     const double self_kv = (double)B * (t + 2) * 2 * d * L;
-    return 4.0 * (weights + cross + self_kv + (double)B * V);
+    const double kvb = kv24() ? 3.0 : 4.0;
+    return 4.0 * (weights + (double)B * V) + kvb * (cross + self_kv);
   }
   double decode_step_flops(int B, int t) const {
     const double d = cfg.d_model, ff = cfg.d_ff, L = cfg.n_layers, V = cfg.vocab;

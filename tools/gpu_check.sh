@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 TAG=${1:-check}
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread \
   > gpurun_out/${TAG}_tests.log 2>&1 || { echo "TESTS FAILED"; tail -40 gpurun_out/${TAG}_tests.log; exit 1; }
 tail -3 gpurun_out/${TAG}_tests.log
 timeout -k 10 120 python -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/${TAG}_smoke.log 2>&1 \
