@@ -5,7 +5,7 @@ class's summed kernel time.  Usage: python tools/trace_overlap.py run_kernel_tra
 import csv
 import sys
 
-DEC = ("foldgemm", "dec_", "rowgemm", "beam_")
+DEC = ("foldgemm", "foldwide", "dec_", "rowgemm", "beam_")
 
 
 def main(path):
