@@ -1111,8 +1111,11 @@ struct mocr_engine {
 
   void gemm(const char* name, Operand A, Operand Wt, const float* bias, float* C, uint16_t* Ch, uint16_t* Cl,
             int Mrows, int N, int K, int epi, const WinGeom* wg, long alg_rows, int col_split = 0,
-            size_t split_stride = 0) {
+            size_t split_stride = 0, uint16_t* kv16 = nullptr, uint8_t* kv8 = nullptr, int kv_M = 0) {
     GemmParams p{};
+    p.kv16 = kv16;
+    p.kv8 = kv8;
+    p.kv_M = kv_M;
     if (bf16_mode()) {
       p.A = A.hi;
       p.A_lo = A.lo;
@@ -1305,9 +1308,13 @@ struct mocr_engine {
     }
     gemm("memproj", opX, wop(lay->projw), W(lay->projb), MEM, MEMh, MEMl, B * M, (int)d, kEncDim, EPI_STORE, nullptr,
          (long)B * M);
-    gemm("crosskv", Operand{MEM, MEMh, MEMl}, Operand{kvw_all, kvwh, kvwl}, kvb_all, MEMKV, nullptr, nullptr, B * M,
-         (int)(L * 2 * d), (int)d, EPI_STORE, nullptr, (long)B * M, (int)(2 * d), (size_t)cfg.max_batch * M * 2 * d);
-    split_memkv24(B);
+    // bf16x3 greedy engines: the epilogue writes the fp24 planes the step streams (no fp32
+    // copy unless beam search, whose kernels read fp32, may run on this engine)
+    const bool kv_planes = kv24() && bf16_mode();
+    gemm("crosskv", Operand{MEM, MEMh, MEMl}, Operand{kvw_all, kvwh, kvwl}, kvb_all,
+         kv_planes && cfg.max_beam == 0 ? nullptr : MEMKV, nullptr, nullptr, B * M, (int)(L * 2 * d), (int)d,
+         EPI_STORE, nullptr, (long)B * M, (int)(2 * d), (size_t)cfg.max_batch * M * 2 * d,
+         kv_planes ? MEMKV16 : nullptr, kv_planes ? MEMKV8 : nullptr, M);
     MOCR_HIP_CHECK(hipStreamSynchronize(stream));
     if (timing) flush_timing();
     encoded = true;
@@ -1971,6 +1978,22 @@ int mocr_set_cu_mask(mocr_engine* eng, const uint32_t* mask, int n_words) {
       MOCR_HIP_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)n_words, mask));
     else
       MOCR_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    MOCR_HIP_CHECK(hipStreamDestroy(eng->stream));
+    eng->stream = s;
+  })
+}
+
+int mocr_set_stream_priority(mocr_engine* eng, int priority) {
+  MOCR_API_BODY(eng, {
+    MOCR_HIP_CHECK(hipSetDevice(eng->device));
+    int least = 0;
+    int greatest = 0;
+    MOCR_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    // priority: 0 normal, > 0 higher (the device's greatest), < 0 lower (its least)
+    const int prio = priority > 0 ? greatest : (priority < 0 ? least : 0);
+    MOCR_HIP_CHECK(hipStreamSynchronize(eng->stream));
+    hipStream_t s = nullptr;
+    MOCR_HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio));
     MOCR_HIP_CHECK(hipStreamDestroy(eng->stream));
     eng->stream = s;
   })

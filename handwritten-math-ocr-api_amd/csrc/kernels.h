@@ -55,6 +55,12 @@ struct GemmParams {
   ConvGeom conv;       // conv.on: A is the implicit im2col of an NHWC map (bf16 planes)
   const void* zero;    // >= 64 zero bytes (conv padding taps)
   int force_kernel;    // 0: the dispatch's choice; tools/gemm_bench A/B: launch_gemm_bf16 kKernel*
+  // EPI_STORE with col_split (gemm_bf16 only): also write the output as the greedy step's
+  // fp24 cross-attention K/V planes (common.h), head-major [col block][row / kv_M][k | v]
+  // [8 heads][kv_M][32] per block (col_split = 512); C may then be null
+  uint16_t* kv16;
+  uint8_t* kv8;
+  int kv_M;
 };
 
 void launch_gemm_f32(const GemmParams& p, hipStream_t s);

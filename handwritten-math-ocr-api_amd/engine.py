@@ -82,6 +82,7 @@ def load_library(path: str = LIB_PATH):
         "mocr_set_timing": (I, [P, I]),
         "mocr_get_timing": (I, [P, ctypes.POINTER(KernelStat), I]),
         "mocr_set_cu_mask": (I, [P, ctypes.POINTER(ctypes.c_uint32), I]),
+        "mocr_set_stream_priority": (I, [P, I]),
         "mocr_group_unique_id": (I, [ctypes.c_char_p]),
         "mocr_group_create": (I, [ctypes.c_char_p, I, I, I, ctypes.POINTER(P)]),
         "mocr_group_destroy": (I, [P]),
@@ -119,7 +120,7 @@ def exported_symbols():
     return ["mocr_abi_version", "mocr_source_hash", "mocr_device_count", "mocr_weight_count", "mocr_memory_tokens", "mocr_create", "mocr_destroy",
             "mocr_last_error", "mocr_load_weights", "mocr_set_images", "mocr_set_images_device", "mocr_encode",
             "mocr_get_memory", "mocr_decode", "mocr_decode_device", "mocr_decode_beam", "mocr_debug_encode_until",
-            "mocr_set_timing", "mocr_get_timing", "mocr_set_encoder_pos", "mocr_set_cu_mask", "mocr_group_unique_id", "mocr_group_create",
+            "mocr_set_timing", "mocr_get_timing", "mocr_set_encoder_pos", "mocr_set_cu_mask", "mocr_set_stream_priority", "mocr_group_unique_id", "mocr_group_create",
             "mocr_group_destroy", "mocr_group_last_error", "mocr_group_gather_ids"]
 
 
@@ -330,6 +331,11 @@ class Engine:
         for c in cus:
             arr[c // 32] |= 1 << (c % 32)
         self._check(self.lib.mocr_set_cu_mask(self._h, arr, words), "mocr_set_cu_mask")
+
+    def set_stream_priority(self, priority: int):
+        """Recreate the engine's stream at the device's highest (> 0), lowest (< 0) or the
+        normal (0) HIP stream priority."""
+        self._check(self.lib.mocr_set_stream_priority(self._h, int(priority)), "mocr_set_stream_priority")
 
     # ------------------------------------------------------------------ timing
     def set_timing(self, enabled: bool):

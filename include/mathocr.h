@@ -208,6 +208,10 @@ int mocr_set_timing(mocr_engine* eng, int enabled); /* also resets the counters 
 /* Restrict the engine's HIP stream to a set of CUs (hipExtStreamCreateWithCUMask: bit i
  * of mask[i / 32] enables CU i); n_words = 0 restores an unmasked stream. */
 int mocr_set_cu_mask(mocr_engine* eng, const uint32_t* mask, int n_words);
+
+/* Recreate the engine's stream at a HIP stream priority: > 0 the device's highest, < 0
+ * its lowest, 0 normal (pipeline experiments: a decode chain above a concurrent encoder). */
+int mocr_set_stream_priority(mocr_engine* eng, int priority);
 int mocr_get_timing(mocr_engine* eng, mocr_kernel_stat* out, int max_records);
 
 /* ---- Image-parallel group (BASELINE config 3) ----------------

@@ -21,6 +21,8 @@ ap.add_argument("--cus", default="256,224,192")
 ap.add_argument("--ne", type=int, default=6)
 ap.add_argument("--nd", type=int, default=4)
 ap.add_argument("--rows", type=int, default=256)
+ap.add_argument("--dec-priority", type=int, default=0, help="decoder stream priority (> 0 high, < 0 low)")
+ap.add_argument("--enc-priority", type=int, default=0)
 a = ap.parse_args()
 pkg = importlib.import_module("handwritten-math-ocr-api_amd")
 R, S = a.rows, 128
@@ -33,6 +35,8 @@ for r in range(2):
     e.encode()
     engs.append(e)
 ids = torch.empty((R, S + 1), dtype=torch.int32, device="cuda:0")
+engs[0].set_stream_priority(a.enc_priority)
+engs[1].set_stream_priority(a.dec_priority)
 engs[1].decode_into(ids, max_steps=S, stop="none")
 torch.cuda.synchronize()
 
@@ -61,13 +65,14 @@ def run(fns):
 
 
 for n in [int(x) for x in a.cus.split(",")]:
-    engs[0].set_cu_mask(None if n >= 256 else range(n))
+    if n < 256:
+        engs[0].set_cu_mask(range(n))
     run([enc_loop])
     e_alone = run([enc_loop])[0]
     d_alone = run([dec_loop])[0]
     e_tog, d_tog = run([enc_loop, dec_loop])
     imgs = R * (a.ne + a.nd)
-    print(json.dumps({"enc_cus": n, "enc_alone_ms": e_alone, "dec_alone_ms": d_alone, "enc_together_ms": e_tog,
+    print(json.dumps({"enc_cus": n, "dec_priority": a.dec_priority, "enc_priority": a.enc_priority, "enc_alone_ms": e_alone, "dec_alone_ms": d_alone, "enc_together_ms": e_tog,
                       "dec_together_ms": d_tog, "overlap": round((e_alone + d_alone - max(e_tog, d_tog)) /
                                                                  min(e_alone, d_alone), 3),
                       "img_s_together": round(R * a.ne / (max(e_tog, d_tog) / 1e3) * 0 + imgs / 2 / (max(e_tog, d_tog) / 1e3), 1)}),
