@@ -31,6 +31,7 @@ constexpr int kHeads[kStages] = {3, 6, 12, 24};
 constexpr int kEmbed = 96;
 constexpr int kEncDim = 768;
 constexpr int kDecodeChunk = 8;  // steps per captured graph
+constexpr int kSyncStopRows = 16;  // batch-stop check after every chunk up to this many rows (decode())
 
 struct StageGeom {
   int H, W, C, heads;
@@ -1699,6 +1700,12 @@ struct mocr_engine {
     // Batch stop: the state after chunk c is copied to a pinned slot behind chunk c, and
     // the host checks chunk c - 1's copy only once chunk c is queued, so the GPU never
     // idles between chunks; a chunk launched after the stop skips every step (dec_skip).
+    // Up to kSyncStopRows rows (serving: im2latex.predict, predict.py) the host waits for
+    // chunk c's own state before queuing chunk c + 1: a stop then wastes at most the rest
+    // of its chunk instead of up to two chunks of early-out launches (B = 1, EOS at step
+    // 1: 2.39 ms for the deferred check, tools/stop_batch_probe.py), for a host round trip
+    // per chunk.
+    const bool sync_stop = stop_batch && B <= kSyncStopRows;
     for (int c = 0; c < chunks; ++c) {
       hipGraphExec_t ge = graph_for(B, c, max_steps, want_logits, forced_host != nullptr, stop_batch);
       const auto h0 = std::chrono::steady_clock::now();
@@ -1712,9 +1719,10 @@ struct mocr_engine {
       if (stop_batch && c + 1 < chunks) {
         MOCR_HIP_CHECK(hipMemcpyAsync(&st_host[c & 1], st, sizeof(DecodeState), hipMemcpyDeviceToHost, stream));
         MOCR_HIP_CHECK(hipEventRecord(chunk_ev[c & 1], stream));
-        if (c > 0) {
-          MOCR_HIP_CHECK(hipEventSynchronize(chunk_ev[(c - 1) & 1]));
-          if (st_host[(c - 1) & 1].done_step != 0x7fffffff) break;
+        const int cc = sync_stop ? c : c - 1;  // the chunk whose state is checked now
+        if (cc >= 0) {
+          MOCR_HIP_CHECK(hipEventSynchronize(chunk_ev[cc & 1]));
+          if (st_host[cc & 1].done_step != 0x7fffffff) break;
         }
       }
     }
