@@ -31,39 +31,39 @@ __device__ __forceinline__ floatx4 ld_stream4(const float* p) {
 }
 
 // fp24 K/V storage of the greedy decode (bf16x3 engines): an fp32 rounded to nearest at
-// bit 8 keeps sign, exponent and 15 mantissa bits (relative error <= 2^-16), held as a
-// 16-bit plane (bits 31..16) and an 8-bit plane (bits 15..8): 3 of 4 bytes streamed per
-// step.  On the CPU oracle, K/V rounded this way move teacher-forced logits by <= 1.8e-5
+// bit 8 keeps sign, exponent and 15 mantissa bits (relative error <= 2^-16).  Packed in
+// 12-byte groups of 4 consecutive elements: their upper 16 bits (4 x 2 B), then bits
+// 15..8 (4 x 1 B), so element e of a buffer sits in group e / 4 at byte 12 (e / 4) and a
+// lane's 4 elements are one 12-byte (dwordx3) load: 3 of 4 bytes streamed per step.
+// On the CPU oracle, K/V rounded this way move teacher-forced logits by <= 1.8e-5
 // (tests/probes/kv16_probe.py), the size of the bf16x3 GEMMs' own rounding.
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 __device__ __forceinline__ uint32_t fp24_bits(float x) { return (__float_as_uint(x) + 0x80u) >> 8; }
-__device__ __forceinline__ float fp24_value(uint32_t hi16, uint32_t mid8) {
-  return __uint_as_float((hi16 << 16) | (mid8 << 8));
-}
 __device__ __forceinline__ float fp24_round(float x) { return __uint_as_float(fp24_bits(x) << 8); }
-// 4 consecutive elements: 8 B of the 16-bit plane, 4 B of the 8-bit plane
-__device__ __forceinline__ floatx4 fp24_unpack4(uint2 h, uint32_t m) {
+__device__ __forceinline__ floatx4 fp24_unpack4(u32x3 w) {
   floatx4 v;
-  v[0] = __uint_as_float((h.x << 16) | ((m & 0xffu) << 8));
-  v[1] = __uint_as_float((h.x & 0xffff0000u) | (m & 0xff00u));
-  v[2] = __uint_as_float((h.y << 16) | ((m >> 8) & 0xff00u));
-  v[3] = __uint_as_float((h.y & 0xffff0000u) | ((m >> 16) & 0xff00u));
+  v[0] = __uint_as_float((w[0] << 16) | ((w[2] & 0xffu) << 8));
+  v[1] = __uint_as_float((w[0] & 0xffff0000u) | (w[2] & 0xff00u));
+  v[2] = __uint_as_float((w[1] << 16) | ((w[2] >> 8) & 0xff00u));
+  v[3] = __uint_as_float((w[1] & 0xffff0000u) | ((w[2] >> 16) & 0xff00u));
   return v;
 }
-__device__ __forceinline__ floatx4 ld_stream_fp24x4(const uint16_t* hi, const uint8_t* mid) {
-  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+// the 4 elements e .. e + 3 (e % 4 == 0) of a packed buffer
+__device__ __forceinline__ floatx4 ld_stream_fp24x4(const uint8_t* base, size_t e) {
+  const u32x3* p = reinterpret_cast<const u32x3*>(base + 3 * e);
 #if MOCR_KV_NT
-  const u32x2 h = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(hi));
-  const uint32_t m = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(mid));
+  return fp24_unpack4(__builtin_nontemporal_load(p));
 #else
-  const u32x2 h = *reinterpret_cast<const u32x2*>(hi);
-  const uint32_t m = *reinterpret_cast<const uint32_t*>(mid);
+  return fp24_unpack4(*p);
 #endif
-  return fp24_unpack4(make_uint2(h[0], h[1]), m);
 }
-__device__ __forceinline__ void st_fp24x4(uint16_t* hi, uint8_t* mid, const floatx4& v) {
+__device__ __forceinline__ void st_fp24x4(uint8_t* base, size_t e, const floatx4& v) {
   const uint32_t r0 = fp24_bits(v[0]), r1 = fp24_bits(v[1]), r2 = fp24_bits(v[2]), r3 = fp24_bits(v[3]);
-  *reinterpret_cast<uint2*>(hi) = make_uint2((r0 >> 8) | ((r1 >> 8) << 16), (r2 >> 8) | ((r3 >> 8) << 16));
-  *reinterpret_cast<uint32_t*>(mid) = (r0 & 0xffu) | ((r1 & 0xffu) << 8) | ((r2 & 0xffu) << 16) | ((r3 & 0xffu) << 24);
+  u32x3 w;
+  w[0] = (r0 >> 8) | ((r1 >> 8) << 16);
+  w[1] = (r2 >> 8) | ((r3 >> 8) << 16);
+  w[2] = (r0 & 0xffu) | ((r1 & 0xffu) << 8) | ((r2 & 0xffu) << 16) | ((r3 & 0xffu) << 24);
+  *reinterpret_cast<u32x3*>(base + 3 * e) = w;
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -309,8 +309,8 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
     const int m = m_first + it * 4 * RPW;
     const size_t o = kvb + (size_t)(m < n_cached ? m : 0) * kvr;  // row 0 is allocated; masked below
     if constexpr (F24) {
-      kk[it] = ld_stream_fp24x4(p.K16 + o, p.K8 + o);
-      vv[it] = ld_stream_fp24x4(p.V16 + o, p.V8 + o);
+      kk[it] = ld_stream_fp24x4(p.K24, o);
+      vv[it] = ld_stream_fp24x4(p.V24, o);
     } else {
       kk[it] = ld_stream4(p.K + o);
       vv[it] = ld_stream4(p.V + o);
@@ -377,8 +377,8 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
     if (wave == 0 && rsub == 0 && !dec_skip(p.st, t)) {
       if constexpr (F24) {
         const size_t o = kvb + (size_t)t * 32;
-        st_fp24x4(p.kc16 + o, p.kc8 + o, zv[1]);
-        st_fp24x4(p.vc16 + o, p.vc8 + o, zv[2]);
+        st_fp24x4(p.kc24, o, zv[1]);
+        st_fp24x4(p.vc24, o, zv[2]);
       } else {
         const size_t o = kvb + (size_t)t * p.kv_row_stride;
         *reinterpret_cast<floatx4*>(p.kcache + o) = zv[1];
@@ -506,9 +506,9 @@ void launch_dec_foldattn(const FoldAttnParams& p, bool self_attn, hipStream_t s)
   if (p.sel_on && (!self_attn || zs || !p.qtab || !p.qpos || !p.emb || !p.pos || !p.x || p.sel.t != p.t - 1 ||
                    (p.sel.part && p.sel.nparts > 512)))
     throw std::runtime_error("foldattn: the selection runs in layer 0's self-attention of step sel.t + 1");
-  const bool f24 = p.K16 != nullptr;
-  if (f24 && (!p.K8 || !p.V16 || !p.V8 || (self_attn && (!p.kc16 || !p.kc8 || !p.vc16 || !p.vc8))))
-    throw std::runtime_error("foldattn: fp24 K/V needs both planes of K and V (and of the cache)");
+  const bool f24 = p.K24 != nullptr;
+  if (f24 && (!p.V24 || (self_attn && (!p.kc24 || !p.vc24))))
+    throw std::runtime_error("foldattn: fp24 K/V needs K and V (and the cache)");
   if (p.B <= 0) return;
   const int nit = (p.n + 31) / 32;  // 32 key rows per workgroup pass (4 waves x 8 rows)
   const dim3 grid(p.B, kD / 32);

@@ -316,10 +316,9 @@ struct mocr_engine {
   float *ds_sa = nullptr, *ds_ca = nullptr, *ds_ff = nullptr;  // row-stat partials [B][16][2]
   float* dlogits_hist = nullptr;
   float *kcache = nullptr, *vcache = nullptr;
-  // fp24 planes (common.h) of the cross-attention K/V and of the self-attention cache that
-  // the folded greedy step streams in bf16x3 engines (kv24())
-  uint16_t *MEMKV16 = nullptr, *kc16 = nullptr, *vc16 = nullptr;
-  uint8_t *MEMKV8 = nullptr, *kc8 = nullptr, *vc8 = nullptr;
+  // packed fp24 (common.h) cross-attention K/V and self-attention cache that the folded
+  // greedy step streams in bf16x3 engines (kv24()); 3 bytes per element
+  uint8_t *MEMKV24 = nullptr, *kc24 = nullptr, *vc24 = nullptr;
   int32_t *ids = nullptr, *feed = nullptr, *forced = nullptr, *finished = nullptr;
   float* logp = nullptr;
   DecodeState* st = nullptr;
@@ -380,7 +379,7 @@ struct mocr_engine {
                     ds_sa,   ds_ca,   ds_ff,
                     dlogits_hist, kcache, vcache, ids, feed, forced, finished, logp, st, XWh, XWl, ATTh, ATTl,
                     HIDh, HIDl, MEMh, MEMl, dwh, dwl, kvwh, kvwl, bscore, bfin, bseq[0], bseq[1],
-                    bslot[0], bslot[1], fold_buf, qtab, qpos, dzqkv, dpart, MEMKV16, MEMKV8, kc16, kc8, vc16, vc8};
+                    bslot[0], bslot[1], fold_buf, qtab, qpos, dzqkv, dpart, MEMKV24, kc24, vc24};
     for (void* p : bufs)
       if (p) (void)hipFree(p);
     for (void* p : frag_allocs)
@@ -763,12 +762,9 @@ struct mocr_engine {
     vcache = dalloc<float>(L * R * cfg.max_pos * d);
     if (kv24()) {
       const size_t nkv = (size_t)B * M * L * 2 * d, nc = L * R * cfg.max_pos * d;
-      MEMKV16 = dalloc<uint16_t>(nkv);
-      MEMKV8 = dalloc<uint8_t>(nkv);
-      kc16 = dalloc<uint16_t>(nc);
-      kc8 = dalloc<uint8_t>(nc);
-      vc16 = dalloc<uint16_t>(nc);
-      vc8 = dalloc<uint8_t>(nc);
+      MEMKV24 = dalloc<uint8_t>(3 * nkv);
+      kc24 = dalloc<uint8_t>(3 * nc);
+      vc24 = dalloc<uint8_t>(3 * nc);
     }
     ld_ids = cfg.max_pos + 1;
     if (cfg.max_beam > 0) {
@@ -1071,7 +1067,7 @@ struct mocr_engine {
     const size_t kv_layer = (size_t)cfg.max_batch * M * 2 * d;
     timed("memkv(fp24)", 0, 7.0 * cfg.n_layers * (double)B * M * 2 * d, [&] {
       for (int l = 0; l < cfg.n_layers; ++l)
-        launch_split_kv_fp24(MEMKV + l * kv_layer, MEMKV16 + l * kv_layer, MEMKV8 + l * kv_layer, B, M, stream);
+        launch_split_kv_fp24(MEMKV + l * kv_layer, MEMKV24 + 3 * l * kv_layer, B, M, stream);
     });
   }
   // the wide logits on bf16x3 MFMA (fc_out planes) in bf16x3 engines unless MOCR_VARIANT_LOGITS_F32
@@ -1112,10 +1108,9 @@ struct mocr_engine {
 
   void gemm(const char* name, Operand A, Operand Wt, const float* bias, float* C, uint16_t* Ch, uint16_t* Cl,
             int Mrows, int N, int K, int epi, const WinGeom* wg, long alg_rows, int col_split = 0,
-            size_t split_stride = 0, uint16_t* kv16 = nullptr, uint8_t* kv8 = nullptr, int kv_M = 0) {
+            size_t split_stride = 0, uint8_t* kv24 = nullptr, int kv_M = 0) {
     GemmParams p{};
-    p.kv16 = kv16;
-    p.kv8 = kv8;
+    p.kv24 = kv24;
     p.kv_M = kv_M;
     if (bf16_mode()) {
       p.A = A.hi;
@@ -1315,7 +1310,7 @@ struct mocr_engine {
     gemm("crosskv", Operand{MEM, MEMh, MEMl}, Operand{kvw_all, kvwh, kvwl}, kvb_all,
          kv_planes && cfg.max_beam == 0 ? nullptr : MEMKV, nullptr, nullptr, B * M, (int)(L * 2 * d), (int)d,
          EPI_STORE, nullptr, (long)B * M, (int)(2 * d), (size_t)cfg.max_batch * M * 2 * d,
-         kv_planes ? MEMKV16 : nullptr, kv_planes ? MEMKV8 : nullptr, M);
+         kv_planes ? MEMKV24 : nullptr, M);
     MOCR_HIP_CHECK(hipStreamSynchronize(stream));
     if (timing) flush_timing();
     encoded = true;
@@ -1473,7 +1468,7 @@ struct mocr_engine {
       a.K = kc; a.V = vc; a.kcache = kc; a.vcache = vc;
       if (kv24()) {  // head-major [rows][8][max_pos][32] per layer
         const size_t o = l * cache_layer;
-        a.K16 = a.kc16 = kc16 + o; a.K8 = a.kc8 = kc8 + o; a.V16 = a.vc16 = vc16 + o; a.V8 = a.vc8 = vc8 + o;
+        a.K24 = a.kc24 = kc24 + 3 * o; a.V24 = a.vc24 = vc24 + 3 * o;
         a.f24_b = (size_t)8 * cfg.max_pos * 32; a.f24_h = (size_t)cfg.max_pos * 32;
       }
       a.kv_b_stride = (size_t)cfg.max_pos * d; a.kv_row_stride = d; a.n = t + 1;
@@ -1493,7 +1488,7 @@ struct mocr_engine {
       a.K = memk; a.V = memk + d; a.kv_b_stride = (size_t)M * 2 * d; a.kv_row_stride = 2 * d; a.n = M;
       if (kv24()) {  // head-major [B][k | v][8][M][32] per layer
         const size_t o = l * kv_layer, ov = o + (size_t)8 * M * 32;
-        a.K16 = MEMKV16 + o; a.K8 = MEMKV8 + o; a.V16 = MEMKV16 + ov; a.V8 = MEMKV8 + ov;
+        a.K24 = MEMKV24 + 3 * o; a.V24 = MEMKV24 + 3 * ov;
         a.f24_b = (size_t)2 * 8 * M * 32; a.f24_h = (size_t)M * 32;
       }
       launch_dec_foldattn(a, false, s);

@@ -333,14 +333,14 @@ __device__ __forceinline__ void epi_vec8(const GemmParams& p, int row, int col, 
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
     }
     const size_t off = (size_t)row * p.ldc + col;
-    if (EPI == EPI_STORE && p.kv16) {  // fp24 K/V planes, 8 columns of one head
+    if (EPI == EPI_STORE && p.kv24) {  // packed fp24 K/V, 8 columns of one head
       const int blk = col / p.col_split;
       const int c = col - blk * p.col_split;
       const int b = row / p.kv_M;
       const size_t o = blk * p.split_stride + ((size_t)(b * 2 + (c >> 8)) * 8 + ((c >> 5) & 7)) * p.kv_M * 32 +
                        (size_t)(row - b * p.kv_M) * 32 + (c & 31);
-      st_fp24x4(p.kv16 + o, p.kv8 + o, floatx4{v[0], v[1], v[2], v[3]});
-      st_fp24x4(p.kv16 + o + 4, p.kv8 + o + 4, floatx4{v[4], v[5], v[6], v[7]});
+      st_fp24x4(p.kv24, o, floatx4{v[0], v[1], v[2], v[3]});
+      st_fp24x4(p.kv24, o + 4, floatx4{v[4], v[5], v[6], v[7]});
     }
     if (p.C) {
       float* c = p.C + off;

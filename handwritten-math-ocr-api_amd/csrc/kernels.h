@@ -56,10 +56,9 @@ struct GemmParams {
   const void* zero;    // >= 64 zero bytes (conv padding taps)
   int force_kernel;    // 0: the dispatch's choice; tools/gemm_bench A/B: launch_gemm_bf16 kKernel*
   // EPI_STORE with col_split (gemm_bf16 only): also write the output as the greedy step's
-  // fp24 cross-attention K/V planes (common.h), head-major [col block][row / kv_M][k | v]
-  // [8 heads][kv_M][32] per block (col_split = 512); C may then be null
-  uint16_t* kv16;
-  uint8_t* kv8;
+  // packed fp24 cross-attention K/V (common.h), head-major [col block][row / kv_M][k | v]
+  // [8 heads][kv_M][32] elements per block (col_split = 512); C may then be null
+  uint8_t* kv24;
   int kv_M;
 };
 
@@ -144,10 +143,9 @@ void launch_swin_attn_noproj(const SwinAttnParams& p, hipStream_t s);
 
 // x -> bf16 hi (and lo) planes.
 void launch_split_bf16(const float* x, uint16_t* hi, uint16_t* lo, size_t n, hipStream_t s);
-// Cross-attention K/V [rows = B * M][2 * 256] fp32 -> fp24 planes (common.h fp24_*: 16-bit
-// plane of bits 31..16, 8-bit plane of bits 15..8 after rounding at bit 8), head-major
-// [B][k | v][8 heads][M][32] (FoldAttnParams f24_*)
-void launch_split_kv_fp24(const float* kv, uint16_t* hi, uint8_t* mid, int B, int M, hipStream_t s);
+// Cross-attention K/V [rows = B * M][2 * 256] fp32 -> packed fp24 (common.h fp24_*),
+// head-major [B][k | v][8 heads][M][32] elements (FoldAttnParams f24_*)
+void launch_split_kv_fp24(const float* kv, uint8_t* kv24, int B, int M, hipStream_t s);
 
 // ------------------------------------------------------------------ decoder
 // Every decode kernel takes its step index t as an argument (one captured graph per
@@ -266,13 +264,12 @@ struct FoldAttnParams {
   const float* K;
   const float* V;
   float *kcache, *vcache;  // self only: this layer's cache (same strides as K/V)
-  // fp24 K/V (common.h): the planes replace K / V / kcache / vcache when K16 is set.  Head-
-  // major: key m of head h of row b at b * f24_b + h * f24_h + 32 m (a head's 32 columns
-  // of consecutive keys are adjacent, so the 16- and 8-bit loads fill whole lines)
-  const uint16_t *K16, *V16;
-  const uint8_t *K8, *V8;
-  uint16_t *kc16, *vc16;
-  uint8_t *kc8, *vc8;
+  // packed fp24 K/V (common.h): replace K / V / kcache / vcache when K24 is set.  Head-
+  // major: key m of head h of row b at element b * f24_b + h * f24_h + 32 m (a head's
+  // keys are adjacent: each lane's 4 columns are one 12-byte load, 8 key rows of a wave
+  // instruction 768 contiguous bytes)
+  const uint8_t *K24, *V24;
+  uint8_t *kc24, *vc24;
   size_t f24_b, f24_h;
   size_t kv_b_stride;
   int kv_row_stride;

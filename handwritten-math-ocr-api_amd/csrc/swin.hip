@@ -573,8 +573,7 @@ __global__ void split_bf16_kernel(const float* __restrict__ x, RowOut out, size_
 }
 
 // cross K/V fp32 [B * M][512] -> fp24 head-major planes [B][2][8][M][32], 4 columns per thread
-__global__ void split_kv_fp24_kernel(const float* __restrict__ kv, uint16_t* __restrict__ hi, uint8_t* __restrict__ mid,
-                                     int M, size_t n4) {
+__global__ void split_kv_fp24_kernel(const float* __restrict__ kv, uint8_t* __restrict__ kv24, int M, size_t n4) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (; i < n4; i += stride) {
@@ -583,7 +582,7 @@ __global__ void split_kv_fp24_kernel(const float* __restrict__ kv, uint16_t* __r
     const size_t b = row / M;
     const int m = (int)(row - b * M);
     const size_t o = ((b * 2 + (col >> 8)) * 8 + ((col >> 5) & 7)) * (size_t)M * 32 + (size_t)m * 32 + (col & 31);
-    st_fp24x4(hi + o, mid + o, reinterpret_cast<const floatx4*>(kv)[i]);
+    st_fp24x4(kv24, o, reinterpret_cast<const floatx4*>(kv)[i]);
   }
 }
 
@@ -652,11 +651,11 @@ void launch_window_attention(const float* QKV, const float* relbias, const float
   MOCR_HIP_CHECK(hipGetLastError());
 }
 
-void launch_split_kv_fp24(const float* kv, uint16_t* hi, uint8_t* mid, int B, int M, hipStream_t s) {
+void launch_split_kv_fp24(const float* kv, uint8_t* kv24, int B, int M, hipStream_t s) {
   const size_t n4 = (size_t)B * M * 128;
   if (n4 == 0) return;
   const unsigned blocks = (unsigned)std::min<size_t>((n4 + 255) / 256, 65536);
-  split_kv_fp24_kernel<<<blocks, 256, 0, s>>>(kv, hi, mid, M, n4);
+  split_kv_fp24_kernel<<<blocks, 256, 0, s>>>(kv, kv24, M, n4);
   MOCR_HIP_CHECK(hipGetLastError());
 }
 
