@@ -66,6 +66,21 @@ __device__ __forceinline__ void st_fp24x4(uint8_t* base, size_t e, const floatx4
   *reinterpret_cast<u32x3*>(base + 3 * e) = w;
 }
 
+// int16 cross-attention K/V (bf16x3 greedy engines): one scale per (row, column) over the
+// memory's keys, k = q * scale (tests/probes/kv16_probe.py: logits move <= 1.6e-5, as fp24).
+// The 4 elements e .. e + 3 (e % 4 == 0) as one 8-byte load, not yet scaled.
+__device__ __forceinline__ floatx4 ld_stream_i16x4(const int16_t* base, size_t e) {
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2* p = reinterpret_cast<const u32x2*>(base + e);
+#if MOCR_KV_NT
+  const u32x2 w = __builtin_nontemporal_load(p);
+#else
+  const u32x2 w = *p;
+#endif
+  return floatx4{(float)(int16_t)(w[0] & 0xffffu), (float)((int32_t)w[0] >> 16), (float)(int16_t)(w[1] & 0xffffu),
+                 (float)((int32_t)w[1] >> 16)};
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -280,11 +280,15 @@ __global__ void __launch_bounds__(64 * NW) foldgemm_kernel(FoldGemmParams p) {
 // t-1 for its row (select.h; the head-0 workgroup does the bookkeeping), then takes q|k|v
 // of the selected token from the tables and writes its 32 columns of x = emb + pos --
 // the work of a separate argmax kernel at the end of step t-1, without its launch.
-// F24: K/V (and the self-attention cache) in fp24 planes (common.h).
-template <bool SELF, bool ZS, bool SEL, int NIT, bool F24>
+// KVF: K/V (and the self-attention cache) in fp32 (0) or fp24 planes (1, common.h); 2:
+// cross-attention K/V in int16 with per-column scales (the scales of K fold into q, those
+// of V into the output).
+template <bool SELF, bool ZS, bool SEL, int NIT, int KVF>
 __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   constexpr int LPR = 8;  // lanes per key row
   constexpr int RPW = 8;  // key rows per wave instruction
+  constexpr bool F24 = KVF == 1, I16 = KVF == 2;
+  static_assert(!(SELF && I16), "int16 K/V: cross-attention only");
   __shared__ floatx4 po[4][LPR];
   __shared__ float pm[4], ps[4];
 
@@ -301,8 +305,8 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   const int n_cached = SELF ? t : n;
   const int m_first = wave * RPW + rsub;
 
-  const size_t kvb = F24 ? (size_t)b * p.f24_b + (size_t)h * p.f24_h + li * 4 : (size_t)b * p.kv_b_stride + cc;
-  const size_t kvr = F24 ? 32 : (size_t)p.kv_row_stride;
+  const size_t kvb = KVF ? (size_t)b * p.f24_b + (size_t)h * p.f24_h + li * 4 : (size_t)b * p.kv_b_stride + cc;
+  const size_t kvr = KVF ? 32 : (size_t)p.kv_row_stride;
   floatx4 kk[NIT], vv[NIT];
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
@@ -311,6 +315,9 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
     if constexpr (F24) {
       kk[it] = ld_stream_fp24x4(p.K24, o);
       vv[it] = ld_stream_fp24x4(p.V24, o);
+    } else if constexpr (I16) {
+      kk[it] = ld_stream_i16x4(p.K16, o);
+      vv[it] = ld_stream_i16x4(p.V16, o);
     } else {
       kk[it] = ld_stream4(p.K + o);
       vv[it] = ld_stream4(p.V + o);
@@ -354,7 +361,12 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) zv[j][e] = fmaf(rstd, fmaf(-mean, sv[j][e], zv[j][e]), cv[j][e]);
   }
-  const floatx4 q4 = zv[0];
+  floatx4 q4 = zv[0];
+  floatx4 vs4;
+  if constexpr (I16) {
+    q4 *= *reinterpret_cast<const floatx4*>(p.Ks + (size_t)b * p.s_b + cc);
+    vs4 = *reinterpret_cast<const floatx4*>(p.Vs + (size_t)b * p.s_b + cc);
+  }
   const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
   if constexpr (SELF && F24) {  // the newest key / value as every later step reads them from the cache
 #pragma unroll
@@ -417,6 +429,7 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   sum = xsum8_16_32(sum);
 #pragma unroll
   for (int e = 0; e < 4; ++e) o4[e] = xsum8_16_32(o4[e]);
+  if constexpr (I16) o4 *= vs4;
   if (rsub == 0) {
     po[wave][li] = o4;
     if (li == 0) {
@@ -506,9 +519,11 @@ void launch_dec_foldattn(const FoldAttnParams& p, bool self_attn, hipStream_t s)
   if (p.sel_on && (!self_attn || zs || !p.qtab || !p.qpos || !p.emb || !p.pos || !p.x || p.sel.t != p.t - 1 ||
                    (p.sel.part && p.sel.nparts > 512)))
     throw std::runtime_error("foldattn: the selection runs in layer 0's self-attention of step sel.t + 1");
-  const bool f24 = p.K24 != nullptr;
+  const bool f24 = p.K24 != nullptr, i16 = p.K16 != nullptr;
   if (f24 && (!p.V24 || (self_attn && (!p.kc24 || !p.vc24))))
     throw std::runtime_error("foldattn: fp24 K/V needs K and V (and the cache)");
+  if (i16 && (self_attn || f24 || !p.V16 || !p.Ks || !p.Vs || p.s_b < kD))
+    throw std::runtime_error("foldattn: int16 K/V is cross-attention only, with K, V and their scales");
   if (p.B <= 0) return;
   const int nit = (p.n + 31) / 32;  // 32 key rows per workgroup pass (4 waves x 8 rows)
   const dim3 grid(p.B, kD / 32);
@@ -523,13 +538,18 @@ void launch_dec_foldattn(const FoldAttnParams& p, bool self_attn, hipStream_t s)
     dec_foldattn_kernel<false, true, false, N, F><<<grid, 256, 0, s>>>(p); \
   else                                                                     \
     dec_foldattn_kernel<false, false, false, N, F><<<grid, 256, 0, s>>>(p);
-#define MOCR_FA(N)          \
-  case N:                   \
-    if (f24) {              \
-      MOCR_FA2(N, true)     \
-    } else {                \
-      MOCR_FA2(N, false)    \
-    }                       \
+#define MOCR_FA(N)                                                        \
+  case N:                                                                 \
+    if (i16) {                                                            \
+      if (zs)                                                             \
+        dec_foldattn_kernel<false, true, false, N, 2><<<grid, 256, 0, s>>>(p);  \
+      else                                                                \
+        dec_foldattn_kernel<false, false, false, N, 2><<<grid, 256, 0, s>>>(p); \
+    } else if (f24) {                                                     \
+      MOCR_FA2(N, 1)                                                      \
+    } else {                                                              \
+      MOCR_FA2(N, 0)                                                      \
+    }                                                                     \
     break;
   switch (nit) {
     MOCR_FA(1) MOCR_FA(2) MOCR_FA(3) MOCR_FA(4) MOCR_FA(5) MOCR_FA(6) MOCR_FA(7) MOCR_FA(8) MOCR_FA(9)

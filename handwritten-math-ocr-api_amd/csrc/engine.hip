@@ -236,7 +236,8 @@ void check_config(const mocr_config& c) {
       "precision");
   req((c.variant & ~(MOCR_VARIANT_UNFUSED_ATTN | MOCR_VARIANT_UNFUSED_MLP | MOCR_VARIANT_DEC_UNFOLDED |
                       MOCR_VARIANT_S4_FUSED_ATTN | MOCR_VARIANT_WINDOW_ROWS | MOCR_VARIANT_DEC_NARROW |
-                      MOCR_VARIANT_LOGITS_F32 | MOCR_VARIANT_S3_LARGE_BATCH | MOCR_VARIANT_KV_F32)) == 0,
+                      MOCR_VARIANT_LOGITS_F32 | MOCR_VARIANT_S3_LARGE_BATCH | MOCR_VARIANT_KV_F32 |
+                      MOCR_VARIANT_CROSS_KV_F24)) == 0,
       "variant: unknown MOCR_VARIANT_* flag");
   req(c.sos_id >= 0 && c.sos_id < c.vocab && c.eos_id >= 0 && c.eos_id < c.vocab, "special ids");
 }
@@ -319,6 +320,10 @@ struct mocr_engine {
   // packed fp24 (common.h) cross-attention K/V and self-attention cache that the folded
   // greedy step streams in bf16x3 engines (kv24()); 3 bytes per element
   uint8_t *MEMKV24 = nullptr, *kc24 = nullptr, *vc24 = nullptr;
+  // int16 cross-attention K/V (kvx16(), replaces the fp24 planes of MEMKV24) and its
+  // per-(layer, row, column) scales [L][max_batch][2d]
+  int16_t* MEMKV16 = nullptr;
+  float* MEMKVS = nullptr;
   int32_t *ids = nullptr, *feed = nullptr, *forced = nullptr, *finished = nullptr;
   float* logp = nullptr;
   DecodeState* st = nullptr;
@@ -379,7 +384,7 @@ struct mocr_engine {
                     ds_sa,   ds_ca,   ds_ff,
                     dlogits_hist, kcache, vcache, ids, feed, forced, finished, logp, st, XWh, XWl, ATTh, ATTl,
                     HIDh, HIDl, MEMh, MEMl, dwh, dwl, kvwh, kvwl, bscore, bfin, bseq[0], bseq[1],
-                    bslot[0], bslot[1], fold_buf, qtab, qpos, dzqkv, dpart, MEMKV24, kc24, vc24};
+                    bslot[0], bslot[1], fold_buf, qtab, qpos, dzqkv, dpart, MEMKV24, kc24, vc24, MEMKV16, MEMKVS};
     for (void* p : bufs)
       if (p) (void)hipFree(p);
     for (void* p : frag_allocs)
@@ -762,7 +767,12 @@ struct mocr_engine {
     vcache = dalloc<float>(L * R * cfg.max_pos * d);
     if (kv24()) {
       const size_t nkv = (size_t)B * M * L * 2 * d, nc = L * R * cfg.max_pos * d;
-      MEMKV24 = dalloc<uint8_t>(3 * nkv);
+      if (kvx16()) {
+        MEMKV16 = dalloc<int16_t>(nkv);
+        MEMKVS = dalloc<float>((size_t)L * B * 2 * d);
+      } else {
+        MEMKV24 = dalloc<uint8_t>(3 * nkv);
+      }
       kc24 = dalloc<uint8_t>(3 * nc);
       vc24 = dalloc<uint8_t>(3 * nc);
     }
@@ -1060,11 +1070,21 @@ struct mocr_engine {
   bool kv24() const {
     return fold_greedy() && cfg.precision == MOCR_PRECISION_BF16X3 && !(cfg.variant & MOCR_VARIANT_KV_F32);
   }
-  // the fp24 planes of the cross-attention K/V of the B encoded images
+  // ... with the cross-attention K/V in int16 and per-column scales, unless
+  // MOCR_VARIANT_CROSS_KV_F24 (fp24 as the self-attention cache)
+  bool kvx16() const { return kv24() && !(cfg.variant & MOCR_VARIANT_CROSS_KV_F24); }
+  // the int16 (or fp24) cross-attention K/V of the B encoded images from MEMKV
   void split_memkv24(int B) {
     if (!kv24()) return;
     const int d = cfg.d_model;
     const size_t kv_layer = (size_t)cfg.max_batch * M * 2 * d;
+    if (kvx16()) {
+      timed("memkv(i16)", 0, 6.0 * cfg.n_layers * (double)B * M * 2 * d, [&] {
+        launch_quant_kv_i16(MEMKV, MEMKV16, MEMKVS, B, M, cfg.n_layers, kv_layer, (size_t)cfg.max_batch * 2 * d,
+                            stream);
+      });
+      return;
+    }
     timed("memkv(fp24)", 0, 7.0 * cfg.n_layers * (double)B * M * 2 * d, [&] {
       for (int l = 0; l < cfg.n_layers; ++l)
         launch_split_kv_fp24(MEMKV + l * kv_layer, MEMKV24 + 3 * l * kv_layer, B, M, stream);
@@ -1306,11 +1326,12 @@ struct mocr_engine {
          (long)B * M);
     // bf16x3 greedy engines: the epilogue writes the fp24 planes the step streams (no fp32
     // copy unless beam search, whose kernels read fp32, may run on this engine)
-    const bool kv_planes = kv24() && bf16_mode();
+    const bool kv_planes = kv24() && bf16_mode() && !kvx16();
     gemm("crosskv", Operand{MEM, MEMh, MEMl}, Operand{kvw_all, kvwh, kvwl}, kvb_all,
          kv_planes && cfg.max_beam == 0 ? nullptr : MEMKV, nullptr, nullptr, B * M, (int)(L * 2 * d), (int)d,
          EPI_STORE, nullptr, (long)B * M, (int)(2 * d), (size_t)cfg.max_batch * M * 2 * d,
          kv_planes ? MEMKV24 : nullptr, M);
+    if (kvx16()) split_memkv24(B);
     MOCR_HIP_CHECK(hipStreamSynchronize(stream));
     if (timing) flush_timing();
     encoded = true;
@@ -1488,7 +1509,12 @@ struct mocr_engine {
       a.K = memk; a.V = memk + d; a.kv_b_stride = (size_t)M * 2 * d; a.kv_row_stride = 2 * d; a.n = M;
       if (kv24()) {  // head-major [B][k | v][8][M][32] per layer
         const size_t o = l * kv_layer, ov = o + (size_t)8 * M * 32;
-        a.K24 = MEMKV24 + 3 * o; a.V24 = MEMKV24 + 3 * ov;
+        if (kvx16()) {
+          a.K16 = MEMKV16 + o; a.V16 = MEMKV16 + ov;
+          a.Ks = MEMKVS + (size_t)l * cfg.max_batch * 2 * d; a.Vs = a.Ks + d; a.s_b = 2 * d;
+        } else {
+          a.K24 = MEMKV24 + 3 * o; a.V24 = MEMKV24 + 3 * ov;
+        }
         a.f24_b = (size_t)2 * 8 * M * 32; a.f24_h = (size_t)M * 32;
       }
       launch_dec_foldattn(a, false, s);
@@ -1753,8 +1779,8 @@ struct mocr_engine {
     const double weights = L * (6 * d * d + 2 * d * ff) + V * d;
     const double cross = (double)B * M * 2 * d * L;
     const double self_kv = (double)B * (t + 2) * 2 * d * L;
-    const double kvb = kv24() ? 3.0 : 4.0;
-    return 4.0 * (weights + (double)B * V) + kvb * (cross + self_kv);
+    const double kvb = kv24() ? 3.0 : 4.0, kvx = kvx16() ? 2.0 : kvb;
+    return 4.0 * (weights + (double)B * V) + kvx * cross + kvb * self_kv;
   }
   double decode_step_flops(int B, int t) const {
     const double d = cfg.d_model, ff = cfg.d_ff, L = cfg.n_layers, V = cfg.vocab;

@@ -146,6 +146,11 @@ void launch_split_bf16(const float* x, uint16_t* hi, uint16_t* lo, size_t n, hip
 // Cross-attention K/V [rows = B * M][2 * 256] fp32 -> packed fp24 (common.h fp24_*),
 // head-major [B][k | v][8 heads][M][32] elements (FoldAttnParams f24_*)
 void launch_split_kv_fp24(const float* kv, uint8_t* kv24, int B, int M, hipStream_t s);
+// Cross-attention K/V of L layers [L][layer_stride elements] fp32 -> int16 in the same
+// head-major order, with scale[l][b][512] = max over the M keys of |column| / 32767
+// (common.h ld_stream_i16x4; FoldAttnParams K16)
+void launch_quant_kv_i16(const float* kv, int16_t* q, float* scale, int B, int M, int L, size_t layer_stride,
+                         size_t scale_stride, hipStream_t s);
 
 // ------------------------------------------------------------------ decoder
 // Every decode kernel takes its step index t as an argument (one captured graph per
@@ -271,6 +276,11 @@ struct FoldAttnParams {
   const uint8_t *K24, *V24;
   uint8_t *kc24, *vc24;
   size_t f24_b, f24_h;
+  // cross-attention only: int16 K/V in the same head-major order (f24_b, f24_h), scaled
+  // per (row, column): K = K16 * Ks[b * s_b + column], V = V16 * Vs[...]
+  const int16_t *K16, *V16;
+  const float *Ks, *Vs;
+  int s_b;
   size_t kv_b_stride;
   int kv_row_stride;
   int n;                   // keys (self: t + 1)

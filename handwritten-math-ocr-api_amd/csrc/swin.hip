@@ -586,6 +586,34 @@ __global__ void split_kv_fp24_kernel(const float* __restrict__ kv, uint8_t* __re
   }
 }
 
+// cross K/V fp32 [B * M][512] -> int16 head-major [B][2][8][M][32] with one scale per (b,
+// column) over the M keys; one workgroup per (b, layer), 2 columns per thread
+__global__ void __launch_bounds__(256) quant_kv_i16_kernel(const float* __restrict__ kv, int16_t* __restrict__ q,
+                                                           float* __restrict__ scale, int M, size_t layer_stride,
+                                                           size_t scale_stride) {
+  const int b = blockIdx.x;
+  const int c = threadIdx.x * 2;
+  const float* src = kv + blockIdx.y * layer_stride + (size_t)b * M * 512 + c;
+  float a0 = 0.f, a1 = 0.f;
+#pragma unroll 8
+  for (int m = 0; m < M; ++m) {
+    const float2 v = *reinterpret_cast<const float2*>(src + (size_t)m * 512);
+    a0 = fmaxf(a0, fabsf(v.x));
+    a1 = fmaxf(a1, fabsf(v.y));
+  }
+  const float i0 = a0 > 0.f ? 32767.f / a0 : 0.f, i1 = a1 > 0.f ? 32767.f / a1 : 0.f;
+  *reinterpret_cast<float2*>(scale + blockIdx.y * scale_stride + (size_t)b * 512 + c) =
+      float2{a0 > 0.f ? a0 / 32767.f : 1.f, a1 > 0.f ? a1 / 32767.f : 1.f};
+  int16_t* dst = q + blockIdx.y * layer_stride + ((size_t)(b * 2 + (c >> 8)) * 8 + ((c >> 5) & 7)) * M * 32 + (c & 31);
+#pragma unroll 8
+  for (int m = 0; m < M; ++m) {
+    const float2 v = *reinterpret_cast<const float2*>(src + (size_t)m * 512);
+    const int r0 = max(-32767, min(32767, (int)rintf(v.x * i0)));
+    const int r1 = max(-32767, min(32767, (int)rintf(v.y * i1)));
+    *reinterpret_cast<uint32_t*>(dst + (size_t)m * 32) = ((uint32_t)r0 & 0xffffu) | ((uint32_t)r1 << 16);
+  }
+}
+
 inline unsigned blocks_for_rows(long rows) { return (unsigned)((rows + 3) / 4); }
 
 }  // namespace
@@ -656,6 +684,15 @@ void launch_split_kv_fp24(const float* kv, uint8_t* kv24, int B, int M, hipStrea
   if (n4 == 0) return;
   const unsigned blocks = (unsigned)std::min<size_t>((n4 + 255) / 256, 65536);
   split_kv_fp24_kernel<<<blocks, 256, 0, s>>>(kv, kv24, M, n4);
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_quant_kv_i16(const float* kv, int16_t* q, float* scale, int B, int M, int L, size_t layer_stride,
+                         size_t scale_stride, hipStream_t s) {
+  if (B <= 0 || L <= 0) return;
+  if (M <= 0 || scale_stride < (size_t)B * 512 || layer_stride < (size_t)B * M * 512)
+    throw std::runtime_error("quant_kv_i16: bad strides");
+  quant_kv_i16_kernel<<<dim3(B, L), 256, 0, s>>>(kv, q, scale, M, layer_stride, scale_stride);
   MOCR_HIP_CHECK(hipGetLastError());
 }
 

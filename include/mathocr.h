@@ -85,8 +85,11 @@ enum {
   MOCR_VARIANT_S3_LARGE_BATCH = 128, /* Swin stage 3 takes its >= 128-image kernels at any batch     */
                                      /* (unfused attention over the image tokens, mlp.hip's fused    */
                                      /* C = 384 MLP), so small-batch parity tests cover that path    */
-  MOCR_VARIANT_KV_F32 = 256          /* bf16x3 engines: the greedy step streams fp32 K/V instead of  */
-                                     /* fp24 (16 + 8-bit planes, relative rounding <= 2^-16)         */
+  MOCR_VARIANT_KV_F32 = 256,         /* bf16x3 engines: the greedy step streams fp32 K/V instead of  */
+                                     /* fp24 (packed 16 + 8 bits, relative rounding <= 2^-16) and    */
+                                     /* int16 cross-attention K/V                                    */
+  MOCR_VARIANT_CROSS_KV_F24 = 512    /* bf16x3 engines: cross-attention K/V in fp24 instead of int16 */
+                                     /* with one scale per (row, column) over the memory's keys      */
 };
 
 /* Greedy stopping rule (src/inference.py:23-25). */

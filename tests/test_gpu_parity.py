@@ -120,7 +120,7 @@ def test_teacher_forced_logits_384(pkg, g384):
     np.testing.assert_array_equal(res.ids[:, 1:], g["ids"][:, 1:])
 
 
-@pytest.mark.parametrize("variant", [(), ("logits_f32",), ("kv_f32",)])
+@pytest.mark.parametrize("variant", [(), ("logits_f32",), ("kv_f32",), ("cross_kv_f24",)])
 @pytest.mark.parametrize("name", ["g384_b2_pert", "g96x320_b4_eos"])
 def test_teacher_forced_logits_bf16x3(pkg, golden, name, variant):
     """The bench precision (bf16x3 encoder GEMMs, attention, fold GEMMs and logits of the

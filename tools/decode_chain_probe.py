@@ -26,6 +26,7 @@ ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--steps", type=int, default=128)
 ap.add_argument("--precision", default="bf16x3")
 ap.add_argument("--lib", default=None)
+ap.add_argument("--variant", default="", help="comma-separated engine.VARIANT names")
 a = ap.parse_args()
 pkg = importlib.import_module("handwritten-math-ocr-api_amd")
 if a.lib:
@@ -37,7 +38,8 @@ for rows in [int(x) for x in a.rows.split(",")]:
     for R in [int(x) for x in a.chains.split(",")]:
         engs, bufs = [], []
         for r in range(R):
-            e = pkg.Engine(img_hw=(384, 384), max_batch=rows, precision=a.precision, device=0)
+            e = pkg.Engine(img_hw=(384, 384), max_batch=rows, precision=a.precision, device=0,
+                           variant=tuple(v for v in a.variant.split(",") if v))
             e.load_weights(w)
             e.set_images(torch.from_numpy(pkg.synth.make_images(rows, 384, 384, seed0=1000 + r * rows)).to("cuda:0"))
             e.encode()
