@@ -1128,10 +1128,14 @@ struct mocr_engine {
 
   void gemm(const char* name, Operand A, Operand Wt, const float* bias, float* C, uint16_t* Ch, uint16_t* Cl,
             int Mrows, int N, int K, int epi, const WinGeom* wg, long alg_rows, int col_split = 0,
-            size_t split_stride = 0, uint8_t* kv24 = nullptr, int kv_M = 0) {
+            size_t split_stride = 0, uint8_t* kv24 = nullptr, int kv_M = 0, int16_t* kv16 = nullptr,
+            float* kv16_scale = nullptr, size_t kv16_sstride = 0) {
     GemmParams p{};
     p.kv24 = kv24;
     p.kv_M = kv_M;
+    p.kv16 = kv16;
+    p.kv16_scale = kv16_scale;
+    p.kv16_sstride = kv16_sstride;
     if (bf16_mode()) {
       p.A = A.hi;
       p.A_lo = A.lo;
@@ -1326,12 +1330,18 @@ struct mocr_engine {
          (long)B * M);
     // bf16x3 greedy engines: the epilogue writes the fp24 planes the step streams (no fp32
     // copy unless beam search, whose kernels read fp32, may run on this engine)
+    // (int16 K/V: quantised in the epilogue when each 144-row half tile is one image and
+    // beam search, whose kernels read fp32, cannot run on this engine; else by a pass over
+    // the fp32 output)
     const bool kv_planes = kv24() && bf16_mode() && !kvx16();
+    const bool kv16_epi = kvx16() && bf16_mode() && M == 144 && cfg.max_beam == 0;
+    const size_t kv_layer = (size_t)cfg.max_batch * M * 2 * d;
     gemm("crosskv", Operand{MEM, MEMh, MEMl}, Operand{kvw_all, kvwh, kvwl}, kvb_all,
-         kv_planes && cfg.max_beam == 0 ? nullptr : MEMKV, nullptr, nullptr, B * M, (int)(L * 2 * d), (int)d,
-         EPI_STORE, nullptr, (long)B * M, (int)(2 * d), (size_t)cfg.max_batch * M * 2 * d,
-         kv_planes ? MEMKV24 : nullptr, M);
-    if (kvx16()) split_memkv24(B);
+         (kv_planes || kv16_epi) && cfg.max_beam == 0 ? nullptr : MEMKV, nullptr, nullptr, B * M, (int)(L * 2 * d),
+         (int)d, kv16_epi ? EPI_KV16 : EPI_STORE, nullptr, (long)B * M, (int)(2 * d), kv_layer,
+         kv_planes ? MEMKV24 : nullptr, M,
+         kv16_epi ? MEMKV16 : nullptr, kv16_epi ? MEMKVS : nullptr, (size_t)cfg.max_batch * 2 * d);
+    if (kvx16() && !kv16_epi) split_memkv24(B);
     MOCR_HIP_CHECK(hipStreamSynchronize(stream));
     if (timing) flush_timing();
     encoded = true;

@@ -265,6 +265,18 @@ __device__ __forceinline__ float gelu_fast(float x) {
 // arithmetic as epi_store element by element, but 16/32-B loads and stores.
 template <int EPI>
 __device__ __forceinline__ void epi_vec8(const GemmParams& p, int row, int col, float (&v)[8]) {
+  if constexpr (EPI == EPI_KV16) {  // int16 K/V: v already biased and quantised (stagq kernel)
+    const int blk = col / p.col_split;
+    const int c = col - blk * p.col_split;
+    const int b = row / p.kv_M;
+    const size_t o = blk * p.split_stride + ((size_t)(b * 2 + (c >> 8)) * 8 + ((c >> 5) & 7)) * p.kv_M * 32 +
+                     (size_t)(row - b * p.kv_M) * 32 + (c & 31);
+    uint32_t w[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w[e] = ((uint32_t)(int)v[2 * e] & 0xffffu) | ((uint32_t)(int)v[2 * e + 1] << 16);
+    *reinterpret_cast<uint4*>(p.kv16 + o) = make_uint4(w[0], w[1], w[2], w[3]);
+    return;
+  }
   if (p.bias) {
     const floatx4 b0 = *reinterpret_cast<const floatx4*>(p.bias + col);
     const floatx4 b1 = *reinterpret_cast<const floatx4*>(p.bias + col + 4);
@@ -941,6 +953,40 @@ __global__ void __launch_bounds__(512) gemm_x3_stagq_kernel(GemmParams p) {
   if (wr == 0) __builtin_amdgcn_s_barrier();  // pair group 1's extra barrier
   __builtin_amdgcn_s_barrier();
 
+  if constexpr (EPI == EPI_KV16) {
+    static_assert(BM == 288, "each wave's 144 rows are one image");
+    {
+      // int16 K/V: this wave's 144 rows are one image; per column, the bias is added, the
+      // max |value| over the image's rows taken (lanes l16 + 16 kq) and the values quantised
+      const int img_row = row0 + wr * (BM / 2);
+#pragma unroll
+      for (int j = 0; j < WTN; ++j) {
+        const int col = col0 + wc * EW + j * 16 + l16;
+        const float bj = p.bias ? p.bias[col] : 0.f;
+        float m = 0.f;
+#pragma unroll
+        for (int i = 0; i < WTM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            acc[i][j][r] += bj;
+            m = fmaxf(m, fabsf(acc[i][j][r]));
+          }
+        m = fmaxf(m, __shfl_xor(m, 16, 64));
+        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        const float inv = m > 0.f ? 32767.f / m : 0.f;
+        if (kq == 0 && img_row < M) {
+          const int blk = col / p.col_split;
+          p.kv16_scale[blk * p.kv16_sstride + (size_t)(img_row / p.kv_M) * p.col_split + (col - blk * p.col_split)] =
+              m > 0.f ? m / 32767.f : 1.f;
+        }
+#pragma unroll
+        for (int i = 0; i < WTM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = fminf(fmaxf(rintf(acc[i][j][r] * inv), -32767.f), 32767.f);
+      }
+    }
+  }
+
   // epilogue: per-wave LDS transpose, ER rows x EW columns per round
   float* ep = reinterpret_cast<float*>(lds) + wave * ER * ES;
 #pragma unroll
@@ -978,6 +1024,12 @@ void launch_stagq(const GemmParams& p, hipStream_t s) {
     case EPI_GELU: gemm_x3_stagq_kernel<EPI_GELU, WTM, WTN, PM, PN><<<grid, 512, 0, s>>>(p); break;
     case EPI_RESADD: gemm_x3_stagq_kernel<EPI_RESADD, WTM, WTN, PM, PN><<<grid, 512, 0, s>>>(p); break;
     case EPI_WINRES: gemm_x3_stagq_kernel<EPI_WINRES, WTM, WTN, PM, PN><<<grid, 512, 0, s>>>(p); break;
+    case EPI_KV16:
+      if constexpr (WTM == 9 && WTN == 4) {
+        gemm_x3_stagq_kernel<EPI_KV16, WTM, WTN, PM, PN><<<grid, 512, 0, s>>>(p);
+        break;
+      }
+      [[fallthrough]];
     default: throw std::runtime_error("gemm_bf16: bad epilogue");
   }
 }
@@ -1096,6 +1148,13 @@ bool try_stagq(const GemmParams& p, hipStream_t s) {
 
 template <int PASSES>
 void launch_bf16_passes(const GemmParams& p, hipStream_t s) {
+  if (p.epi == EPI_KV16) {  // the quantising epilogue lives in the 288 x 256 staggered kernel only
+    if (PASSES != 3 || !p.kv16 || p.C || p.C16 || p.kv24 || p.kv_M != 144 || p.col_split != 512 ||
+        p.N % 512 != 0 || !p.kv16_scale || p.kv16_sstride < (size_t)(p.M / 144) * 512 || p.M % 144 != 0)
+      throw std::runtime_error("gemm_bf16: int16 K/V needs bf16x3, EPI_STORE, no other output, 144-row images, "
+                               "512-column blocks");
+    return launch_stagq<9, 4, 3, 2>(p, s);
+  }
   if (p.force_kernel) return launch_forced<PASSES>(p, s);
   if (try_stagq<PASSES>(p, s)) return;
   if (try_stag<PASSES>(p, s)) return;

@@ -18,6 +18,7 @@ enum Epi : int {
                    // roll(+s), crop)  (torchvision shifted_window_attention tail)
   EPI_RELU = 4,    // C = relu(acc + bias)            (conv + folded BN + ReLU, ResNet BasicBlock)
   EPI_RESRELU = 5, // C = relu(C + (acc + bias))      (BasicBlock: out += identity; relu)
+  EPI_KV16 = 6,    // acc + bias quantised to the int16 cross-attention K/V (GemmParams kv16)
 };
 
 // Implicit-GEMM convolution (gemm_bf16 only): A row m = output pixel (b, oy, ox) of an
@@ -60,6 +61,13 @@ struct GemmParams {
   // [8 heads][kv_M][32] elements per block (col_split = 512); C may then be null
   uint8_t* kv24;
   int kv_M;
+  // ... or as int16 with one scale per (image, column) over its kv_M rows (FoldAttnParams
+  // K16): kv16 in the same head-major order, kv16_scale[col block][row / kv_M][512] at
+  // kv16_sstride floats per block.  EPI_KV16 on the 288 x 256 staggered kernel only,
+  // kv_M = 144 (each wave's 144 rows are one image); C must be null
+  int16_t* kv16;
+  float* kv16_scale;
+  size_t kv16_sstride;
 };
 
 void launch_gemm_f32(const GemmParams& p, hipStream_t s);
