@@ -237,7 +237,7 @@ void check_config(const mocr_config& c) {
   req((c.variant & ~(MOCR_VARIANT_UNFUSED_ATTN | MOCR_VARIANT_UNFUSED_MLP | MOCR_VARIANT_DEC_UNFOLDED |
                       MOCR_VARIANT_S4_FUSED_ATTN | MOCR_VARIANT_WINDOW_ROWS | MOCR_VARIANT_DEC_NARROW |
                       MOCR_VARIANT_LOGITS_F32 | MOCR_VARIANT_S3_LARGE_BATCH | MOCR_VARIANT_KV_F32 |
-                      MOCR_VARIANT_CROSS_KV_F24)) == 0,
+                      MOCR_VARIANT_CROSS_KV_F24 | MOCR_VARIANT_UNFUSED_QKV)) == 0,
       "variant: unknown MOCR_VARIANT_* flag");
   req(c.sos_id >= 0 && c.sos_id < c.vocab && c.eos_id >= 0 && c.eos_id < c.vocab, "special ids");
 }
@@ -1198,6 +1198,7 @@ struct mocr_engine {
     static const char* att_n[] = {"s1.wattn", "s2.wattn", "s3.wattn", "s4.wattn"};
     static const char* mrg_n[] = {"merge1", "merge2", "merge3"};
     static const char* ln1_n[] = {"s1.ln1", "s2.ln1", "s3.ln1", "s4.ln1"};
+    static const char* lnqkv_n[] = {"s1.lnqkv", "s2.lnqkv", "s3.lnqkv", "s4.lnqkv"};
     static const char* ln2_n[] = {"s1.ln2", "s2.ln2", "s3.ln2", "s4.ln2"};
     static const char* mlp_n[] = {"s1.mlp", "s2.mlp", "s3.mlp", "s4.mlp"};
     static const char* attn_n[] = {"s1.attn", "s2.attn", "s3.attn", "s4.attn"};
@@ -1261,10 +1262,20 @@ struct mocr_engine {
           // norm1 and qkv in X's row order, the attention kernel maps window slots to pixels
           // and takes the padded tokens' k / v from the qkv bias, O comes out in X's order,
           // proj is a plain residual-add GEMM (bitwise the window-row sequence below)
-          timed(ln1_n[s], 0, 8.0 * rows * C,
-                [&] { launch_layernorm(X, W(w.n1w), W(w.n1b), xw32, XWh, XWl, (int)rows, C, stream); });
-          gemm(qkv_n[s], opXW, wop(w.qkvw), W(w.qkvb), QKV, nullptr, nullptr, (int)rows, 3 * C, C, EPI_STORE,
-               nullptr, rows);
+          if (C == 384 && s3_large(B) && !(cfg.variant & MOCR_VARIANT_UNFUSED_QKV)) {
+            // norm1 + qkv in one kernel (mlp.hip lngemm384_kernel)
+            LnGemm384Params lp{};
+            lp.X = X; lp.M = rows; lp.ln_g = W(w.n1w); lp.ln_b = W(w.n1b);
+            lp.w = dwh + w.qkvw; lp.wlo = dwl ? dwl + w.qkvw : nullptr; lp.b = W(w.qkvb);
+            lp.out = QKV; lp.N = 3 * C;
+            timed(lnqkv_n[s], 6.0 * rows * C * C, 4.0 * rows * C + 12.0 * rows * C + (dwl ? 4.0 : 2.0) * 3.0 * C * C,
+                  [&] { launch_lngemm384(lp, stream); });
+          } else {
+            timed(ln1_n[s], 0, 8.0 * rows * C,
+                  [&] { launch_layernorm(X, W(w.n1w), W(w.n1b), xw32, XWh, XWl, (int)rows, C, stream); });
+            gemm(qkv_n[s], opXW, wop(w.qkvw), W(w.qkvb), QKV, nullptr, nullptr, (int)rows, 3 * C, C, EPI_STORE,
+                 nullptr, rows);
+          }
           timed(att_n[s], 4.0 * rows * kWinTok * C, 4.0 * (double)rows * 4 * C, [&] {
             launch_window_attention(QKV, relbias[bi], relmask[bi], att32, ATTh, ATTl, B, C, g.heads, wg,
                                     attn_passes(), stream, W(w.qkvb));

@@ -127,6 +127,21 @@ struct MlpParams {
 bool mlp_fused_supported(int C);
 void launch_mlp_fused(const MlpParams& p, hipStream_t s);
 
+// out = LayerNorm(X) W^T + b at C = 384 (mlp.hip lngemm384_kernel): stage 3's norm1 + qkv
+// over the image tokens at >= 128 images, the LN'd rows kept in registers, W streamed
+// through LDS, each 32-column chunk stored when done.  bf16 (wlo null) or bf16x3.
+constexpr int kLnGemm384MaxN = 1152;
+struct LnGemm384Params {
+  const float* X;            // [M, 384]
+  long M;
+  const float *ln_g, *ln_b;  // [384]
+  const void *w, *wlo;       // [N, 384] bf16 hi / lo planes
+  const float* b;            // [N]
+  float* out;                // [M, N]
+  int N;
+};
+void launch_lngemm384(const LnGemm384Params& p, hipStream_t s);
+
 // Fused norm1 + window qkv + W-MSA + proj + residual of one Swin block (wattn.hip),
 // bf16 / bf16x3 (lo planes present) for C = 96, 192 (head dim 32).
 struct SwinAttnParams {

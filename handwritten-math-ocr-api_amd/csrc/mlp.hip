@@ -681,6 +681,184 @@ __global__ void __launch_bounds__(256) mlp384_kernel(MlpParams p) {
   }
 }
 
+
+// ---------------------------------------------------------------- LayerNorm + Linear, C = 384
+// out = LN(X) W^T + b for stage 3's norm1 + qkv over the image tokens at >= 128 images
+// (torchvision SwinTransformerBlock norm1 -> ShiftedWindowAttention's qkv Linear; the
+// attention itself is window_attention_mfma_kernel over `out`).  mlp384_kernel's design
+// without GEMM 2: a wave's 16 TT LN'd rows stay in registers as B fragments, W streams
+// through the same 3-slot LDS-DMA ring a 32-unit chunk at a time (W(jc + 2) issued one
+// piece per k-step while the MFMAs read W(jc)), and every chunk's 32 output columns are
+// stored as soon as they are done, so the output leaves in a steady stream instead of one
+// burst per tile (the GEMM's epilogue), and the LN output never goes through HBM.
+// Chunk rows are permuted as mlp384's W1 (row u = unit pi(u)), so lane group g holds
+// units 8 g .. 8 g + 7 of the chunk: two 16-B stores per row tile.
+template <int PASSES, int TT>
+__global__ void __launch_bounds__(256) lngemm384_kernel(LnGemm384Params p) {
+  constexpr int C = 384, NC = 32, KS1 = C / 32;
+  constexpr bool X3 = PASSES == 3;
+  constexpr int PL = X3 ? 2 : 1;
+  constexpr int PLB = NC * C * 2;             // one plane of a chunk (24 KB)
+  constexpr int NPW = PL * (PLB / 1024) / 4;  // 1-KB DMA pieces per wave and chunk
+  constexpr int NST = 2 * TT;                 // output stores per wave and chunk
+  static_assert(NPW * 4 * 1024 == PL * PLB && NPW <= KS1 && NPW + NST < 64, "DMA split");
+  constexpr int SLOT = PL * PLB;
+  __shared__ __attribute__((aligned(16))) char ring[3 * SLOT];
+  __shared__ __attribute__((aligned(16))) float bs[kLnGemm384MaxN];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j16 = lane & 15;
+  const int g = lane >> 4;
+  const int N = p.N;
+  const int nch = N / NC;
+  const long row0 = (long)blockIdx.x * 64 * TT + wave * 16 * TT;
+  const char* wg[2] = {static_cast<const char*>(p.w), static_cast<const char*>(X3 ? p.wlo : p.w)};
+
+  // piece i of this wave (plane q = i / (NPW / PL)): LDS rows u = 16 h + lane / 4 of k-step
+  // ks's block, unit pi(u) = 8 g + 4 h + (lane / 4) % 4, slot s holds channel chunk s ^ f(g)
+  const uint32_t lb1 = (uint32_t)((8 * g + ((lane >> 2) & 3)) * (C * 2) + (((lane & 3) ^ swz4(lane >> 2)) << 4));
+  auto issue = [&](int jc, char* ws, int i0, int n) {
+    uint32_t lb = lb1;
+    asm volatile("" : "+v"(lb));
+#pragma unroll
+    for (int i = i0; i < i0 + n; ++i) {
+      const int q = i / (NPW / PL);
+      const int rem = (i - q * (NPW / PL)) * 4 + wave;
+      const int ks = rem >> 1, h = rem & 1;
+      const uint32_t off = (uint32_t)((jc * NC + 4 * h) * (C * 2) + ks * 64) + lb;
+      dma16(wg[q], off, lds_u32(ws) + q * PLB + rem * 1024);
+    }
+  };
+  auto slot = [&](int jc) { return ring + (jc % 3) * SLOT; };
+  issue(0, slot(0), 0, NPW);
+  if (nch > 1) issue(1, slot(1), 0, NPW);
+  for (int i = tid; i < N; i += 256) bs[i] = p.b[i];
+
+  // LayerNorm of this wave's TT x 16 rows into the B fragments (lane (g, j): row j of tile
+  // tt, channels 32 ks + 8 g .. + 7); rows >= M repeat row M - 1 (their stores rewrite its
+  // values, so every lane stores and the vmcnt counts below hold)
+  bf16x8 xb[TT][KS1][PL];
+#pragma unroll
+  for (int tt = 0; tt < TT; ++tt) {
+    const long row = min(row0 + tt * 16 + j16, p.M - 1);
+    const float* xr = p.X + (size_t)row * C + 8 * g;
+    float v[KS1][8];
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks) {
+      const floatx4 a = *reinterpret_cast<const floatx4*>(xr + 32 * ks);
+      const floatx4 b = *reinterpret_cast<const floatx4*>(xr + 32 * ks + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[ks][e] = a[e];
+        v[ks][4 + e] = b[e];
+      }
+    }
+    float sm = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sm += v[ks][e];
+    sm = xsum16_32(sm);
+    const float mean = sm / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = v[ks][e] - mean;
+        q += d * d;
+      }
+    q = xsum16_32(q);
+    const float rstd = 1.0f / sqrtf(q / (float)C + 1e-5f);
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks) {
+      const int ch = 32 * ks + 8 * g;
+      const floatx4 g0 = *reinterpret_cast<const floatx4*>(p.ln_g + ch);
+      const floatx4 g1 = *reinterpret_cast<const floatx4*>(p.ln_g + ch + 4);
+      const floatx4 c0 = *reinterpret_cast<const floatx4*>(p.ln_b + ch);
+      const floatx4 c1 = *reinterpret_cast<const floatx4*>(p.ln_b + ch + 4);
+      float y[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        y[e] = (v[ks][e] - mean) * rstd * g0[e] + c0[e];
+        y[4 + e] = (v[ks][4 + e] - mean) * rstd * g1[e] + c1[e];
+      }
+      bf16x8 hi, lo;
+      pack8(y, hi, lo);
+      xb[tt][ks][0] = hi;
+      if constexpr (X3) xb[tt][ks][PL - 1] = lo;
+    }
+    __builtin_amdgcn_sched_barrier(0);  // one row tile's 96 values live at a time
+  }
+  const int fo = j16 * 64 + ((g ^ swz4(j16)) << 4);
+  size_t orow[TT];
+#pragma unroll
+  for (int tt = 0; tt < TT; ++tt) orow[tt] = (size_t)min(row0 + tt * 16 + j16, p.M - 1) * N;
+
+  // W(0) landed (W(1) may stay in flight), then visible to all
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int jc = 0; jc < nch; ++jc) {
+    const bool nxt = jc + 2 < nch;
+    char* s_n = slot(jc + 2);
+    const char* ws = slot(jc);
+    floatx4 acc[2][TT];
+#pragma unroll
+    for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+      for (int tt = 0; tt < TT; ++tt) acc[ht][tt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 fa[2][2][PL];
+    auto rd = [&](int ks, bf16x8(&f)[2][PL]) {
+#pragma unroll
+      for (int ht = 0; ht < 2; ++ht) {
+        const int o = fo + ks * 2048 + ht * 1024;
+        f[ht][0] = *reinterpret_cast<const bf16x8*>(ws + o);
+        if constexpr (X3) f[ht][PL - 1] = *reinterpret_cast<const bf16x8*>(ws + PLB + o);
+      }
+    };
+    rd(0, fa[0]);
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks) {
+      if (ks + 1 < KS1) rd(ks + 1, fa[(ks + 1) & 1]);
+      if (nxt && ks < NPW) issue(jc + 2, s_n, ks, 1);
+#pragma unroll
+      for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+        for (int tt = 0; tt < TT; ++tt) {
+          const bf16x8 ah = fa[ks & 1][ht][0];
+          acc[ht][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, xb[tt][ks][0], acc[ht][tt], 0, 0, 0);
+          if constexpr (X3) {
+            const bf16x8 al = fa[ks & 1][ht][PL - 1];
+            acc[ht][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, xb[tt][ks][1], acc[ht][tt], 0, 0, 0);
+            acc[ht][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, xb[tt][ks][0], acc[ht][tt], 0, 0, 0);
+          }
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // + bias; lane group g: units jc*32 + 8 g + 4 ht + r of row j (tile tt)
+    const int col = jc * NC + 8 * g;
+    const floatx4 bb0 = *reinterpret_cast<const floatx4*>(bs + col);
+    const floatx4 bb1 = *reinterpret_cast<const floatx4*>(bs + col + 4);
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt) {
+      float* o = p.out + orow[tt] + col;
+      __builtin_nontemporal_store(acc[0][tt] + bb0, reinterpret_cast<floatx4*>(o));
+      __builtin_nontemporal_store(acc[1][tt] + bb1, reinterpret_cast<floatx4*>(o + 4));
+    }
+    // W(jc + 1) landed: in issue order W(jc + 2) and stores(jc) may be outstanding behind
+    // it (and stores(jc - 1) is waited for: a per-chunk count that differs in chunk 0 makes
+    // hipcc peel it, 134 VGPRs spilled and 553 vs 499 us per launch at B = 256); then
+    // visible to all, and every wave is past chunk jc, whose slot takes W(jc + 3)
+    if (nxt)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW + NST) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+}
+
 template <int C, int TT, int NC>
 void launch_mlp_c(const MlpParams& p, hipStream_t s) {
   const unsigned grid = (unsigned)((p.M + 128 * TT - 1) / (128 * TT));
@@ -693,6 +871,24 @@ void launch_mlp_c(const MlpParams& p, hipStream_t s) {
 }  // namespace
 
 bool mlp_fused_supported(int C) { return C == 96 || C == 192 || C == 384; }
+
+void launch_lngemm384(const LnGemm384Params& p, hipStream_t s) {
+  if (p.M <= 0) return;
+  if (p.N <= 0 || p.N % 32 != 0 || p.N > kLnGemm384MaxN || !p.X || !p.w || !p.b || !p.out || !p.ln_g || !p.ln_b)
+    throw std::runtime_error("lngemm384: N must be a multiple of 32 up to kLnGemm384MaxN, with every operand");
+  // 128 rows per workgroup (2 row tiles per wave, the LN rows in 192 of the 256 arch VGPRs;
+  // the prologue spills, the chunk loop does not): 1152 workgroups at B = 256
+#ifndef MOCR_LNG_TT
+#define MOCR_LNG_TT 2
+#endif
+  constexpr int TT = MOCR_LNG_TT;
+  const unsigned grid = (unsigned)((p.M + 64 * TT - 1) / (64 * TT));
+  if (p.wlo)
+    lngemm384_kernel<3, TT><<<grid, 256, 0, s>>>(p);
+  else
+    lngemm384_kernel<1, TT><<<grid, 256, 0, s>>>(p);
+  MOCR_HIP_CHECK(hipGetLastError());
+}
 
 void launch_mlp_fused(const MlpParams& p, hipStream_t s) {
   if (p.M <= 0) return;

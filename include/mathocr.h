@@ -88,8 +88,10 @@ enum {
   MOCR_VARIANT_KV_F32 = 256,         /* bf16x3 engines: the greedy step streams fp32 K/V instead of  */
                                      /* fp24 (packed 16 + 8 bits, relative rounding <= 2^-16) and    */
                                      /* int16 cross-attention K/V                                    */
-  MOCR_VARIANT_CROSS_KV_F24 = 512    /* bf16x3 engines: cross-attention K/V in fp24 instead of int16 */
+  MOCR_VARIANT_CROSS_KV_F24 = 512,   /* bf16x3 engines: cross-attention K/V in fp24 instead of int16 */
                                      /* with one scale per (row, column) over the memory's keys      */
+  MOCR_VARIANT_UNFUSED_QKV = 1024    /* stage 3 at >= 128 images: norm1 and the qkv GEMM as two      */
+                                     /* kernels instead of mlp.hip's lngemm384_kernel                */
 };
 
 /* Greedy stopping rule (src/inference.py:23-25). */
