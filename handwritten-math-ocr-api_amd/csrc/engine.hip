@@ -237,7 +237,7 @@ void check_config(const mocr_config& c) {
   req((c.variant & ~(MOCR_VARIANT_UNFUSED_ATTN | MOCR_VARIANT_UNFUSED_MLP | MOCR_VARIANT_DEC_UNFOLDED |
                       MOCR_VARIANT_S4_FUSED_ATTN | MOCR_VARIANT_WINDOW_ROWS | MOCR_VARIANT_DEC_NARROW |
                       MOCR_VARIANT_LOGITS_F32 | MOCR_VARIANT_S3_LARGE_BATCH | MOCR_VARIANT_KV_F32 |
-                      MOCR_VARIANT_CROSS_KV_F24 | MOCR_VARIANT_UNFUSED_QKV)) == 0,
+                      MOCR_VARIANT_CROSS_KV_F24 | MOCR_VARIANT_UNFUSED_LN_GEMM)) == 0,
       "variant: unknown MOCR_VARIANT_* flag");
   req(c.sos_id >= 0 && c.sos_id < c.vocab && c.eos_id >= 0 && c.eos_id < c.vocab, "special ids");
 }
@@ -1262,7 +1262,7 @@ struct mocr_engine {
           // norm1 and qkv in X's row order, the attention kernel maps window slots to pixels
           // and takes the padded tokens' k / v from the qkv bias, O comes out in X's order,
           // proj is a plain residual-add GEMM (bitwise the window-row sequence below)
-          if (C == 384 && s3_large(B) && !(cfg.variant & MOCR_VARIANT_UNFUSED_QKV)) {
+          if (C == 384 && s3_large(B) && !(cfg.variant & MOCR_VARIANT_UNFUSED_LN_GEMM)) {
             // norm1 + qkv in one kernel (mlp.hip lngemm384_kernel)
             LnGemm384Params lp{};
             lp.X = X; lp.M = rows; lp.ln_g = W(w.n1w); lp.ln_b = W(w.n1b);
@@ -1323,10 +1323,20 @@ struct mocr_engine {
       if (s < kStages - 1) {
         const MergeW& m = lay->merge[s];
         const long orow = (long)B * ((g.H + 1) / 2) * ((g.W + 1) / 2);
-        timed(mln_n[s], 0, 8.0 * orow * 4 * C,
-              [&] { launch_merge_ln(X, W(m.nw), W(m.nb), xw32, XWh, XWl, B, g.H, g.W, C, stream); });
-        gemm(mrg_n[s], opXW, wop(m.redw), nullptr, X2, nullptr, nullptr, (int)orow, 2 * C, 4 * C, EPI_STORE, nullptr,
-             orow);
+        if (b16 && 4 * C == 384 && !(cfg.variant & MOCR_VARIANT_UNFUSED_LN_GEMM)) {
+          // gather + norm + reduction in one kernel (mlp.hip lngemm384_kernel)
+          LnGemm384Params lp{};
+          lp.X = X; lp.M = orow; lp.ln_g = W(m.nw); lp.ln_b = W(m.nb);
+          lp.w = dwh + m.redw; lp.wlo = dwl ? dwl + m.redw : nullptr; lp.b = nullptr;
+          lp.out = X2; lp.N = 2 * C; lp.merge_H = g.H; lp.merge_W = g.W;
+          timed(mrg_n[s], 2.0 * orow * 4 * C * 2 * C, 4.0 * (double)B * g.H * g.W * C + 8.0 * orow * C +
+                (dwl ? 4.0 : 2.0) * 8.0 * C * C, [&] { launch_lngemm384(lp, stream); });
+        } else {
+          timed(mln_n[s], 0, 8.0 * orow * 4 * C,
+                [&] { launch_merge_ln(X, W(m.nw), W(m.nb), xw32, XWh, XWl, B, g.H, g.W, C, stream); });
+          gemm(mrg_n[s], opXW, wop(m.redw), nullptr, X2, nullptr, nullptr, (int)orow, 2 * C, 4 * C, EPI_STORE, nullptr,
+               orow);
+        }
         std::swap(X, X2);
         if (stop_after == 2 + 2 * s) return finish_partial(2 + 2 * s);
       }

@@ -128,7 +128,8 @@ bool mlp_fused_supported(int C);
 void launch_mlp_fused(const MlpParams& p, hipStream_t s);
 
 // out = LayerNorm(X) W^T + b at C = 384 (mlp.hip lngemm384_kernel): stage 3's norm1 + qkv
-// over the image tokens at >= 128 images, the LN'd rows kept in registers, W streamed
+// over the image tokens at >= 128 images, and merge 1 (PatchMerging of the 96-channel
+// stage-1 map: gather, norm, reduction), the LN'd rows kept in registers, W streamed
 // through LDS, each 32-column chunk stored when done.  bf16 (wlo null) or bf16x3.
 constexpr int kLnGemm384MaxN = 1152;
 struct LnGemm384Params {
@@ -136,9 +137,11 @@ struct LnGemm384Params {
   long M;
   const float *ln_g, *ln_b;  // [384]
   const void *w, *wlo;       // [N, 384] bf16 hi / lo planes
-  const float* b;            // [N]
+  const float* b;            // [N] or null (no bias)
   float* out;                // [M, N]
   int N;
+  int merge_H, merge_W;      // > 0: X is a [B, H, W, 96] map and row r is PatchMerging's
+                             // 2 x 2 gather of output pixel r (M = B ceil(H/2) ceil(W/2))
 };
 void launch_lngemm384(const LnGemm384Params& p, hipStream_t s);
 

@@ -734,7 +734,7 @@ __global__ void __launch_bounds__(256) lngemm384_kernel(LnGemm384Params p) {
   auto slot = [&](int jc) { return ring + (jc % 3) * SLOT; };
   issue(0, slot(0), 0, NPW);
   if (nch > 1) issue(1, slot(1), 0, NPW);
-  for (int i = tid; i < N; i += 256) bs[i] = p.b[i];
+  for (int i = tid; i < N; i += 256) bs[i] = p.b ? p.b[i] : 0.f;
 
   // LayerNorm of this wave's TT x 16 rows into the B fragments (lane (g, j): row j of tile
   // tt, channels 32 ks + 8 g .. + 7); rows >= M repeat row M - 1 (their stores rewrite its
@@ -743,16 +743,41 @@ __global__ void __launch_bounds__(256) lngemm384_kernel(LnGemm384Params p) {
 #pragma unroll
   for (int tt = 0; tt < TT; ++tt) {
     const long row = min(row0 + tt * 16 + j16, p.M - 1);
-    const float* xr = p.X + (size_t)row * C + 8 * g;
+    // the row's 384 channels: X's row, or PatchMerging's gather [x(0,0), x(1,0), x(0,1),
+    // x(1,1)] of 96 channels each (swin.hip MODE_MERGE; pixels past the map are zeros)
+    const float* src[4];
+    bool valid[4];
+    if (p.merge_H) {
+      const int Ho = (p.merge_H + 1) / 2, Wo = (p.merge_W + 1) / 2;
+      const int bi = (int)(row / ((long)Ho * Wo));
+      const int rem = (int)(row - (long)bi * Ho * Wo);
+      const int oy = rem / Wo, ox = rem - oy * Wo;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int y = 2 * oy + (q & 1), x = 2 * ox + (q >> 1);
+        valid[q] = y < p.merge_H && x < p.merge_W;
+        src[q] = p.X + ((size_t)(bi * p.merge_H + min(y, p.merge_H - 1)) * p.merge_W + min(x, p.merge_W - 1)) * 96;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        valid[q] = true;
+        src[q] = p.X + (size_t)row * C + 96 * q;
+      }
+    }
     float v[KS1][8];
 #pragma unroll
     for (int ks = 0; ks < KS1; ++ks) {
-      const floatx4 a = *reinterpret_cast<const floatx4*>(xr + 32 * ks);
-      const floatx4 b = *reinterpret_cast<const floatx4*>(xr + 32 * ks + 4);
+      const int ch = 32 * ks + 8 * g;
+      const int q = ch / 96;  // lane-dependent piece
+      const float* xr = (q == 0 ? src[0] : q == 1 ? src[1] : q == 2 ? src[2] : src[3]) + (ch - 96 * q);
+      const bool ok = q == 0 ? valid[0] : q == 1 ? valid[1] : q == 2 ? valid[2] : valid[3];
+      const floatx4 a = *reinterpret_cast<const floatx4*>(xr);
+      const floatx4 b = *reinterpret_cast<const floatx4*>(xr + 4);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        v[ks][e] = a[e];
-        v[ks][4 + e] = b[e];
+        v[ks][e] = ok ? a[e] : 0.f;
+        v[ks][4 + e] = ok ? b[e] : 0.f;
       }
     }
     float sm = 0.f;
@@ -874,8 +899,11 @@ bool mlp_fused_supported(int C) { return C == 96 || C == 192 || C == 384; }
 
 void launch_lngemm384(const LnGemm384Params& p, hipStream_t s) {
   if (p.M <= 0) return;
-  if (p.N <= 0 || p.N % 32 != 0 || p.N > kLnGemm384MaxN || !p.X || !p.w || !p.b || !p.out || !p.ln_g || !p.ln_b)
+  if (p.N <= 0 || p.N % 32 != 0 || p.N > kLnGemm384MaxN || !p.X || !p.w || !p.out || !p.ln_g || !p.ln_b)
     throw std::runtime_error("lngemm384: N must be a multiple of 32 up to kLnGemm384MaxN, with every operand");
+  if (p.merge_H && (p.merge_H < 1 || p.merge_W < 1 ||
+                    p.M % ((long)((p.merge_H + 1) / 2) * ((p.merge_W + 1) / 2)) != 0))
+    throw std::runtime_error("lngemm384: PatchMerging rows must be B x ceil(H/2) x ceil(W/2)");
   // 128 rows per workgroup (2 row tiles per wave, the LN rows in 192 of the 256 arch VGPRs;
   // the prologue spills, the chunk loop does not): 1152 workgroups at B = 256
 #ifndef MOCR_LNG_TT

@@ -52,11 +52,13 @@ def test_encoder_stages_match_oracle(pkg, g384):
 
 @pytest.mark.parametrize("variant", [(), ("unfused_attn",), ("unfused_attn", "unfused_mlp"), ("s4_fused_attn",),
                                      ("window_rows",), ("unfused_attn", "window_rows"), ("s3_large_batch",),
-                                     ("s3_large_batch", "unfused_mlp"), ("s3_large_batch", "unfused_qkv")])
+                                     ("s3_large_batch", "unfused_mlp"), ("s3_large_batch", "unfused_ln_gemm"),
+                                     ("unfused_ln_gemm",)])
 def test_bf16x3_encoder_stages_match_oracle(pkg, golden, variant):
     """bf16x3 encoder stage by stage: the fused stage-1/2 attention half (wattn.hip) and
     MLP half (mlp.hip), the stage-3 no-proj kernel, the stage-4 two-half kernel (off in
-    production), stage 3's >= 128-image path (norm1 + qkv in mlp.hip's lngemm384_kernel,
+    production), merge 1 in mlp.hip's lngemm384_kernel, stage 3's >= 128-image path (norm1
+    + qkv in lngemm384_kernel,
     the window attention, mlp.hip's C = 384 fused MLP) and the unfused kernels they replace (MOCR_VARIANT_* flags), all within 1e-4 of
     the fp32 oracle.  384x384: the stage-1 map is 96x96, padded to 98
     (zero tokens) and rolled by 3 on odd blocks."""
