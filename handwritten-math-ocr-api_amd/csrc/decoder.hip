@@ -48,9 +48,10 @@ __device__ __forceinline__ void merge_eq(float& m, float& q, float mb, float qb,
 
 // Cross-lane tree level: this lane's group and its partner's (lane ^ mask) are merged
 // with the lower group first; both lanes get the same result.
-__device__ __forceinline__ void merge_lanes(float& m, float& q, int mask, bool upper, float n) {
-  const float mo = __shfl_xor(m, mask, 64);
-  const float qo = __shfl_xor(q, mask, 64);
+template <int MASK>
+__device__ __forceinline__ void merge_lanes(float& m, float& q, bool upper, float n) {
+  const float mo = lane_partner<MASK>(m);  // lanes.h: DPP for MASK <= 8
+  const float qo = lane_partner<MASK>(q);
   if (upper) {
     float mm = mo, qq = qo;
     merge_eq(mm, qq, m, q, n);
@@ -72,8 +73,8 @@ __device__ __forceinline__ void row_stats_4lanes(const float* __restrict__ part,
   merge_eq(m, q, p0[2], p0[3], 16.f);
   merge_eq(m2, q2, p1[2], p1[3], 16.f);
   merge_eq(m, q, m2, q2, 32.f);
-  merge_lanes(m, q, 16, (g & 1) != 0, 64.f);
-  merge_lanes(m, q, 32, (g & 2) != 0, 128.f);
+  merge_lanes<16>(m, q, (g & 1) != 0, 64.f);
+  merge_lanes<32>(m, q, (g & 2) != 0, 128.f);
   mean = m;
   rstd = rstd_of(q);
 }
@@ -82,10 +83,10 @@ __device__ __forceinline__ void row_stats_4lanes(const float* __restrict__ part,
 // across lanes (lane ^ 1, ^ 2, ^ 4, ^ 8).  Same tree as layout 1.
 __device__ __forceinline__ void row_stats_16lanes(const float* __restrict__ part, int c, float& mean, float& rstd) {
   float m = part[2 * c], q = part[2 * c + 1];
-  merge_lanes(m, q, 1, (c & 1) != 0, 16.f);
-  merge_lanes(m, q, 2, (c & 2) != 0, 32.f);
-  merge_lanes(m, q, 4, (c & 4) != 0, 64.f);
-  merge_lanes(m, q, 8, (c & 8) != 0, 128.f);
+  merge_lanes<1>(m, q, (c & 1) != 0, 16.f);
+  merge_lanes<2>(m, q, (c & 2) != 0, 32.f);
+  merge_lanes<4>(m, q, (c & 4) != 0, 64.f);
+  merge_lanes<8>(m, q, (c & 8) != 0, 128.f);
   mean = m;
   rstd = rstd_of(q);
 }

@@ -22,6 +22,17 @@
 
 namespace mocr {
 
+#ifdef MOCR_FOLD_TS
+// timing probe (tools/build_variant.sh DIR -DMOCR_FOLD_TS, tools/wide_bench.hip): per
+// workgroup, thread 0's clocks at the tile's phase boundaries; slot 0 / 6 the 100-MHz
+// real-time clock at entry / exit, 1..5 the shader clock (see wide_tile)
+__device__ unsigned long long g_fold_ts[8192 * 8];
+#define MOCR_TS(i, v) \
+  if (threadIdx.x == 0 && blockIdx.x < 8192) g_fold_ts[blockIdx.x * 8 + (i)] = (v)
+#else
+#define MOCR_TS(i, v)
+#endif
+
 namespace {
 
 constexpr int kD = 256;
@@ -45,9 +56,10 @@ __device__ __forceinline__ void merge_eq(float& m, float& q, float mb, float qb,
   q = q + qb + delta * delta * (n * 0.5f);
   m = m + delta * 0.5f;
 }
-__device__ __forceinline__ void merge_lanes(float& m, float& q, int mask, bool upper, float n) {
-  const float mo = __shfl_xor(m, mask, 64);
-  const float qo = __shfl_xor(q, mask, 64);
+template <int MASK>
+__device__ __forceinline__ void merge_lanes(float& m, float& q, bool upper, float n) {
+  const float mo = lane_partner<MASK>(m);  // lanes.h: DPP for MASK <= 8
+  const float qo = lane_partner<MASK>(q);
   if (upper) {
     float mm = mo, qq = qo;
     merge_eq(mm, qq, m, q, n);
@@ -70,8 +82,8 @@ __device__ __forceinline__ void merge_part4(const Part4& pp, int g, float& mean,
   merge_eq(m, q, pp.p0[2], pp.p0[3], 16.f);
   merge_eq(m2, q2, pp.p1[2], pp.p1[3], 16.f);
   merge_eq(m, q, m2, q2, 32.f);
-  merge_lanes(m, q, 16, (g & 1) != 0, 64.f);
-  merge_lanes(m, q, 32, (g & 2) != 0, 128.f);
+  merge_lanes<16>(m, q, (g & 1) != 0, 64.f);
+  merge_lanes<32>(m, q, (g & 2) != 0, 128.f);
   mean = m;
   rstd = rstd_of(q);
 }
@@ -81,27 +93,27 @@ __device__ __forceinline__ void merge_part4_quad(const Part4& pp, int g, float& 
   merge_eq(m, q, pp.p0[2], pp.p0[3], 16.f);
   merge_eq(m2, q2, pp.p1[2], pp.p1[3], 16.f);
   merge_eq(m, q, m2, q2, 32.f);
-  merge_lanes(m, q, 1, (g & 1) != 0, 64.f);
-  merge_lanes(m, q, 2, (g & 2) != 0, 128.f);
+  merge_lanes<1>(m, q, (g & 1) != 0, 64.f);
+  merge_lanes<2>(m, q, (g & 2) != 0, 128.f);
   mean = m;
   rstd = rstd_of(q);
 }
 // layout 2 from preloaded (mean, M2) of slice c
 __device__ __forceinline__ void row_stats_16lanes_v(float m, float q, int c, float& mean, float& rstd) {
-  merge_lanes(m, q, 1, (c & 1) != 0, 16.f);
-  merge_lanes(m, q, 2, (c & 2) != 0, 32.f);
-  merge_lanes(m, q, 4, (c & 4) != 0, 64.f);
-  merge_lanes(m, q, 8, (c & 8) != 0, 128.f);
+  merge_lanes<1>(m, q, (c & 1) != 0, 16.f);
+  merge_lanes<2>(m, q, (c & 2) != 0, 32.f);
+  merge_lanes<4>(m, q, (c & 4) != 0, 64.f);
+  merge_lanes<8>(m, q, (c & 8) != 0, 128.f);
   mean = m;
   rstd = rstd_of(q);
 }
 // layout 2: the 16 lanes c = 0..15 of a row each hold slice c
 __device__ __forceinline__ void row_stats_16lanes(const float* __restrict__ part, int c, float& mean, float& rstd) {
   float m = part[2 * c], q = part[2 * c + 1];
-  merge_lanes(m, q, 1, (c & 1) != 0, 16.f);
-  merge_lanes(m, q, 2, (c & 2) != 0, 32.f);
-  merge_lanes(m, q, 4, (c & 4) != 0, 64.f);
-  merge_lanes(m, q, 8, (c & 8) != 0, 128.f);
+  merge_lanes<1>(m, q, (c & 1) != 0, 16.f);
+  merge_lanes<2>(m, q, (c & 2) != 0, 32.f);
+  merge_lanes<4>(m, q, (c & 4) != 0, 64.f);
+  merge_lanes<8>(m, q, (c & 8) != 0, 128.f);
   mean = m;
   rstd = rstd_of(q);
 }
@@ -147,6 +159,8 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
   floatx4* uv_s = reinterpret_cast<floatx4*>(smem);                        // [2][KT / 4]
   char* a_s = smem + L::UV + (threadIdx.x >> 6) * L::AW;                   // this wave's fragments
   float* red = reinterpret_cast<float*>(smem + L::UV + NW * L::AW);       // [NW][BM][BN + 1]
+  MOCR_TS(0, __builtin_amdgcn_s_memrealtime());
+  MOCR_TS(1, __builtin_amdgcn_s_memtime());
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -234,6 +248,10 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
     }
     __syncthreads();
   }
+#ifdef MOCR_FOLD_TS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  MOCR_TS(2, __builtin_amdgcn_s_memtime());
   float m1[MF], rs1[MF], m2[MF], rs2[MF];
 #pragma unroll
   for (int mf = 0; mf < MF; ++mf) {
@@ -322,6 +340,7 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
     }
   }
 
+  MOCR_TS(3, __builtin_amdgcn_s_memtime());
   // ---- combine the 4 waves' partial tiles in a fixed order
   const int g = lane >> 4;
   const int li = lane & 15;
@@ -332,6 +351,7 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
 #pragma unroll
       for (int r = 0; r < 4; ++r) red[(wave * BM + mf * 16 + g * 4 + r) * (BN + 1) + nf * 16 + li] = acc[mf][nf][r];
   __syncthreads();
+  MOCR_TS(4, __builtin_amdgcn_s_memtime());
   if (tid >= 256 || dec_skip(p.st, p.t)) return;
 #pragma unroll
   for (int mf = 0; mf < MF; ++mf) {
@@ -390,6 +410,8 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
       }
     }
   }
+  MOCR_TS(5, __builtin_amdgcn_s_memtime());
+  MOCR_TS(6, __builtin_amdgcn_s_memrealtime());
 }
 
 template <int BM, int BN, int K1, bool S1, bool S2, bool X3, bool LOGITS, int NW>
@@ -526,6 +548,12 @@ void launch_foldwide(const FoldGemmParams& p, hipStream_t s) {
   }
   MOCR_HIP_CHECK(hipGetLastError());
 }
+
+#ifdef MOCR_FOLD_TS
+extern "C" int mocr_debug_fold_ts(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fold_ts), sizeof(unsigned long long) * (size_t)n) == hipSuccess ? 0 : -1;
+}
+#endif
 
 void launch_frag_pack(const float* W, int N, int K, uint16_t* hi, uint16_t* lo, float* f32, hipStream_t s) {
   if (N % 16 != 0 || K % 32 != 0 || (!hi != !lo) || (!hi && !f32)) throw std::runtime_error("frag_pack: N % 16, K % 32");

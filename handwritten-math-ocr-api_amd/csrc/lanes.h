@@ -70,4 +70,18 @@ __device__ __forceinline__ float xsum16_32(float x) {
 __device__ __forceinline__ float xsum8_16_32(float x) { return xsum16_32(x + dpp<0x128>(x)); }
 __device__ __forceinline__ float xmax8_16_32(float x) { return xmax16_32(fmaxf(x, dpp<0x128>(x))); }
 
+// x of lane ^ MASK, for the fixed (mean, M2) merge trees of the decode kernels' LayerNorm
+// statistics, whose level MASK runs after levels 1 .. MASK / 2: MASK = 1, 2 by quad_perm;
+// 4 and 8 by row_half_mirror / row_mirror, which return a lane of the partner quad / half
+// row, all of whose lanes hold the same value by then (so == __shfl_xor); 16, 32 by
+// __shfl_xor (ds_bpermute).
+template <int MASK>
+__device__ __forceinline__ float lane_partner(float x) {
+  if constexpr (MASK == 1) return dpp<0xB1>(x);
+  else if constexpr (MASK == 2) return dpp<0x4E>(x);
+  else if constexpr (MASK == 4) return dpp<0x141>(x);
+  else if constexpr (MASK == 8) return dpp<0x140>(x);
+  else return __shfl_xor(x, MASK, 64);
+}
+
 }  // namespace mocr
