@@ -270,6 +270,16 @@ __global__ void __launch_bounds__(64 * NW) foldgemm_kernel(FoldGemmParams p) {
     fold_tile<(K1 + kD) / (16 * NW), false, S1, S2, NW, X3>(p, (blockIdx.x - kD / 16) * 16);
 }
 
+#ifdef MOCR_FOLD_TS
+// timing probe (tools/attn_ts.hip): thread 0's clocks per workgroup, as decwide.hip's
+__device__ unsigned long long g_attn_ts[8192 * 8];
+#define MOCR_ATS(i, v)                                                             \
+  if (threadIdx.x == 0 && blockIdx.y * gridDim.x + blockIdx.x < 8192)             \
+  g_attn_ts[(blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] = (v)
+#else
+#define MOCR_ATS(i, v)
+#endif
+
 // ------------------------------------------------------------------ fold attention
 // The newest position of row b against n keys for head h (one workgroup, 4 waves): the
 // key loop of decoder.hip dec_attn_kernel (8 lanes per 32-float key row slice, every
@@ -284,14 +294,18 @@ __global__ void __launch_bounds__(64 * NW) foldgemm_kernel(FoldGemmParams p) {
 // KVF: K/V (and the self-attention cache) in fp32 (0) or fp24 planes (1, common.h); 2:
 // cross-attention K/V in int16 with per-column scales (the scales of K fold into q, those
 // of V into the output).
-template <bool SELF, bool ZS, bool SEL, int NIT, int KVF>
+// NW waves (8 key rows each per pass; the selection needs all 4 of its 256 threads).
+template <bool SELF, bool ZS, bool SEL, int NIT, int KVF, int NW>
 __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
+  MOCR_ATS(0, __builtin_amdgcn_s_memrealtime());
+  MOCR_ATS(1, __builtin_amdgcn_s_memtime());
   constexpr int LPR = 8;  // lanes per key row
   constexpr int RPW = 8;  // key rows per wave instruction
   constexpr bool F24 = KVF == 1, I16 = KVF == 2;
   static_assert(!(SELF && I16), "int16 K/V: cross-attention only");
-  __shared__ floatx4 po[4][LPR];
-  __shared__ float pm[4], ps[4];
+  static_assert(!SEL || NW == 4, "the selection runs on 256 threads");
+  __shared__ floatx4 po[NW][LPR];
+  __shared__ float pm[NW], ps[NW];
 
   const int b = blockIdx.x;
   const int h = blockIdx.y;
@@ -311,7 +325,7 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   floatx4 kk[NIT], vv[NIT];
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
-    const int m = m_first + it * 4 * RPW;
+    const int m = m_first + it * NW * RPW;
     const size_t o = kvb + (size_t)(m < n_cached ? m : 0) * kvr;  // row 0 is allocated; masked below
     if constexpr (F24) {
       kk[it] = ld_stream_fp24x4(p.K24, o);
@@ -362,6 +376,10 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) zv[j][e] = fmaf(rstd, fmaf(-mean, sv[j][e], zv[j][e]), cv[j][e]);
   }
+#ifdef MOCR_FOLD_TS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  MOCR_ATS(2, __builtin_amdgcn_s_memtime());
   floatx4 q4 = zv[0];
   floatx4 vs4;
   if constexpr (I16) {
@@ -378,7 +396,7 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   }
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
-    const int m = m_first + it * 4 * RPW;
+    const int m = m_first + it * NW * RPW;
     if constexpr (SELF) {
       kk[it] = m == t ? zv[1] : kk[it];
       vv[it] = m == t ? zv[2] : (m < t ? vv[it] : zero);
@@ -410,7 +428,7 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
     s = fmaf(q4[3], kk[it][3], s);
     s = row_sum<8>(s);  // the 8 lanes of the key row (DPP, as the xor butterfly)
     s *= kAttnScale;
-    sc[it] = (m_first + it * 4 * RPW < n) ? s : -INFINITY;
+    sc[it] = (m_first + it * NW * RPW < n) ? s : -INFINITY;
     mx = fmaxf(mx, sc[it]);
   }
   mx = xmax8_16_32(mx);  // over the wave's 8 key-row groups
@@ -431,6 +449,7 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
 #pragma unroll
   for (int e = 0; e < 4; ++e) o4[e] = xsum8_16_32(o4[e]);
   if constexpr (I16) o4 *= vs4;
+  MOCR_ATS(3, __builtin_amdgcn_s_memtime());
   if (rsub == 0) {
     po[wave][li] = o4;
     if (li == 0) {
@@ -439,19 +458,22 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
     }
   }
   __syncthreads();
+  MOCR_ATS(4, __builtin_amdgcn_s_memtime());
   if (tid < 32 && !dec_skip(p.st, t)) {
     float m = pm[0];
 #pragma unroll
-    for (int w = 1; w < 4; ++w) m = fmaxf(m, pm[w]);
+    for (int w = 1; w < NW; ++w) m = fmaxf(m, pm[w]);
     float num = 0.f, den = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
       const float f = pm[w] == -INFINITY ? 0.f : expf(pm[w] - m);
       num = fmaf(po[w][tid / 4][tid % 4], f, num);
       den = fmaf(ps[w], f, den);
     }
     p.out[(size_t)b * kD + h * 32 + tid] = num / den;
   }
+  MOCR_ATS(5, __builtin_amdgcn_s_memtime());
+  MOCR_ATS(6, __builtin_amdgcn_s_memrealtime());
 }
 
 // ------------------------------------------------------------------ load-time folding
@@ -526,40 +548,63 @@ void launch_dec_foldattn(const FoldAttnParams& p, bool self_attn, hipStream_t s)
   if (i16 && (self_attn || f24 || !p.V16 || !p.Ks || !p.Vs || p.s_b < kD))
     throw std::runtime_error("foldattn: int16 K/V is cross-attention only, with K, V and their scales");
   if (p.B <= 0) return;
-  const int nit = (p.n + 31) / 32;  // 32 key rows per workgroup pass (4 waves x 8 rows)
+  // waves per workgroup: 2 unless the selection runs here (it needs 256 threads) or the
+  // keys exceed 2 x 8 x 10 (tools/attn_ts: the 4-wave kernel's per-wave fixed work --
+  // statistics, unfold, the reductions -- made 8 waves per SIMD VALU-bound)
+#ifndef MOCR_ATTN_WAVES
+#define MOCR_ATTN_WAVES 2
+#endif
+  const int nw = p.waves ? p.waves : ((p.sel_on || p.n > 160) ? 4 : MOCR_ATTN_WAVES);
+  if (nw != 2 && nw != 4) throw std::runtime_error("foldattn: 2 or 4 waves");
+  if (p.sel_on && nw != 4) throw std::runtime_error("foldattn: the selection needs 4 waves");
+  const int nit = (p.n + 8 * nw - 1) / (8 * nw);  // 8 nw key rows per workgroup pass
   const dim3 grid(p.B, kD / 32);
-#define MOCR_FA2(N, F)                                                     \
-  if (self_attn && zs)                                                     \
-    dec_foldattn_kernel<true, true, false, N, F><<<grid, 256, 0, s>>>(p);  \
-  else if (self_attn && p.sel_on)                                          \
-    dec_foldattn_kernel<true, false, true, N, F><<<grid, 256, 0, s>>>(p);  \
-  else if (self_attn)                                                      \
-    dec_foldattn_kernel<true, false, false, N, F><<<grid, 256, 0, s>>>(p); \
-  else if (zs)                                                             \
-    dec_foldattn_kernel<false, true, false, N, F><<<grid, 256, 0, s>>>(p); \
-  else                                                                     \
-    dec_foldattn_kernel<false, false, false, N, F><<<grid, 256, 0, s>>>(p);
-#define MOCR_FA(N)                                                        \
-  case N:                                                                 \
-    if (i16) {                                                            \
-      if (zs)                                                             \
-        dec_foldattn_kernel<false, true, false, N, 2><<<grid, 256, 0, s>>>(p);  \
-      else                                                                \
-        dec_foldattn_kernel<false, false, false, N, 2><<<grid, 256, 0, s>>>(p); \
-    } else if (f24) {                                                     \
-      MOCR_FA2(N, 1)                                                      \
-    } else {                                                              \
-      MOCR_FA2(N, 0)                                                      \
-    }                                                                     \
+#define MOCR_FA2(N, F, W)                                                                  \
+  if (self_attn && zs)                                                                     \
+    dec_foldattn_kernel<true, true, false, N, F, W><<<grid, 64 * W, 0, s>>>(p);           \
+  else if (self_attn && p.sel_on)                                                          \
+    dec_foldattn_kernel<true, false, true, N, F, 4><<<grid, 256, 0, s>>>(p);              \
+  else if (self_attn)                                                                      \
+    dec_foldattn_kernel<true, false, false, N, F, W><<<grid, 64 * W, 0, s>>>(p);          \
+  else if (zs)                                                                             \
+    dec_foldattn_kernel<false, true, false, N, F, W><<<grid, 64 * W, 0, s>>>(p);          \
+  else                                                                                     \
+    dec_foldattn_kernel<false, false, false, N, F, W><<<grid, 64 * W, 0, s>>>(p);
+#define MOCR_FA3(N, W)                                                                     \
+  if (i16) {                                                                               \
+    if (zs)                                                                                \
+      dec_foldattn_kernel<false, true, false, N, 2, W><<<grid, 64 * W, 0, s>>>(p);        \
+    else                                                                                   \
+      dec_foldattn_kernel<false, false, false, N, 2, W><<<grid, 64 * W, 0, s>>>(p);       \
+  } else if (f24) {                                                                        \
+    MOCR_FA2(N, 1, W)                                                                      \
+  } else {                                                                                 \
+    MOCR_FA2(N, 0, W)                                                                      \
+  }
+#define MOCR_FA(N)            \
+  case N:                     \
+    if (nw == 4) {            \
+      MOCR_FA3(N, 4)          \
+    } else if (N <= 10) {     \
+      MOCR_FA3(N, 2)          \
+    }                         \
     break;
+  if (nw == 2 && nit > 10) throw std::runtime_error("foldattn: at most 160 keys on 2 waves");
   switch (nit) {
-    MOCR_FA(1) MOCR_FA(2) MOCR_FA(3) MOCR_FA(4) MOCR_FA(5) MOCR_FA(6) MOCR_FA(7) MOCR_FA(8) MOCR_FA(9)
+    MOCR_FA(1) MOCR_FA(2) MOCR_FA(3) MOCR_FA(4) MOCR_FA(5) MOCR_FA(6) MOCR_FA(7) MOCR_FA(8) MOCR_FA(9) MOCR_FA(10)
     default: throw std::runtime_error("foldattn: at most 288 keys");
   }
 #undef MOCR_FA
+#undef MOCR_FA3
 #undef MOCR_FA2
   MOCR_HIP_CHECK(hipGetLastError());
 }
+
+#ifdef MOCR_FOLD_TS
+extern "C" int mocr_debug_attn_ts(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_attn_ts), sizeof(unsigned long long) * (size_t)n) == hipSuccess ? 0 : -1;
+}
+#endif
 
 void launch_fold_mm(const float* A, int lda, const float* g, const float* Bm, long sbk, long sbj, int K,
                     const float* add_row, const float* add_col, float* out, int ldo, int rows, int cols,

@@ -310,6 +310,7 @@ struct FoldAttnParams {
   size_t kv_b_stride;
   int kv_row_stride;
   int n;                   // keys (self: t + 1)
+  int waves;               // waves per workgroup, 2 or 4 (0: the launcher's choice; tools/attn_ts A/B)
   float* out;              // [B, d]
   int B;
   // layer 0 of step t >= 1: the greedy selection of step t-1 runs here (sel.t = t - 1),

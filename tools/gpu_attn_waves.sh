@@ -1,0 +1,11 @@
+#!/bin/bash
+# decode attention on 2 vs 4 waves per (row, head): phase clocks, parity, decode chain
+set -o pipefail
+O=gpurun_out/aw; mkdir -p $O
+for args in "cross 256 100" "self 256 16" "self 256 60" "self 256 120"; do
+  for w in 4 2; do timeout -k 10 60 ./tools/attn_ts $args $w | head -2 | tail -2 || exit 1; done
+done
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_full.py -m gpu -x -v -rP --timeout 300 --timeout-method thread \
+  -k "teacher_forced or b256_chain or config2 or eos or invariance" > $O/tests.log 2>&1 || { echo "TESTS FAILED"; tail -40 $O/tests.log; exit 1; }
+grep -E "passed|failed|PARITY" $O/tests.log | tail -5
+timeout -k 10 180 python -u tools/decode_chain_probe.py --rows 256 --chains 1,2 --reps 2 2>&1 | grep rows_per_s || exit 1
