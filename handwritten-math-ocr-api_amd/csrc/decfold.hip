@@ -437,7 +437,7 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   if (mx != -INFINITY) {
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
-      const float e = expf(sc[it] - mx);
+      const float e = __expf(sc[it] - mx);  // v_exp_f32 (the libm expf's range reduction is ~10 VALU)
       sum += e;
       o4[0] = fmaf(e, vv[it][0], o4[0]);
       o4[1] = fmaf(e, vv[it][1], o4[1]);
@@ -466,11 +466,11 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
     float num = 0.f, den = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
-      const float f = pm[w] == -INFINITY ? 0.f : expf(pm[w] - m);
+      const float f = pm[w] == -INFINITY ? 0.f : __expf(pm[w] - m);
       num = fmaf(po[w][tid / 4][tid % 4], f, num);
       den = fmaf(ps[w], f, den);
     }
-    p.out[(size_t)b * kD + h * 32 + tid] = num / den;
+    p.out[(size_t)b * kD + h * 32 + tid] = num * __builtin_amdgcn_rcpf(den);
   }
   MOCR_ATS(5, __builtin_amdgcn_s_memtime());
   MOCR_ATS(6, __builtin_amdgcn_s_memrealtime());
@@ -550,12 +550,15 @@ void launch_dec_foldattn(const FoldAttnParams& p, bool self_attn, hipStream_t s)
   if (p.B <= 0) return;
   // waves per workgroup: 2 unless the selection runs here (it needs 256 threads) or the
   // keys exceed 2 x 8 x 10 (tools/attn_ts: the 4-wave kernel's per-wave fixed work --
-  // statistics, unfold, the reductions -- made 8 waves per SIMD VALU-bound)
+  // statistics, unfold, the reductions -- made 8 waves per SIMD VALU-bound: cross 9.9 ->
+  // 8.5 us, self at t = 16 6.9 -> 5.4, t = 120 10.8 -> 10.3)
 #ifndef MOCR_ATTN_WAVES
 #define MOCR_ATTN_WAVES 2
 #endif
-  const int nw = p.waves ? p.waves : ((p.sel_on || p.n > 160) ? 4 : MOCR_ATTN_WAVES);
-  if (nw != 2 && nw != 4) throw std::runtime_error("foldattn: 2 or 4 waves");
+  // (one wave up to 40 keys: self-attention at t = 16 5.42 -> 4.75 us; equal at t = 60,
+  // slower from there and for the 144 memory keys, 8.5 -> 9.3 us)
+  const int nw = p.waves ? p.waves : ((p.sel_on || p.n > 160) ? 4 : (p.n <= 40 ? 1 : MOCR_ATTN_WAVES));
+  if (nw != 1 && nw != 2 && nw != 4) throw std::runtime_error("foldattn: 1, 2 or 4 waves");
   if (p.sel_on && nw != 4) throw std::runtime_error("foldattn: the selection needs 4 waves");
   const int nit = (p.n + 8 * nw - 1) / (8 * nw);  // 8 nw key rows per workgroup pass
   const dim3 grid(p.B, kD / 32);
@@ -581,18 +584,29 @@ void launch_dec_foldattn(const FoldAttnParams& p, bool self_attn, hipStream_t s)
   } else {                                                                                 \
     MOCR_FA2(N, 0, W)                                                                      \
   }
-#define MOCR_FA(N)            \
-  case N:                     \
-    if (nw == 4) {            \
-      MOCR_FA3(N, 4)          \
-    } else if (N <= 10) {     \
-      MOCR_FA3(N, 2)          \
-    }                         \
+#define MOCR_FA(N, W) \
+  case N:               \
+    MOCR_FA3(N, W)      \
     break;
-  if (nw == 2 && nit > 10) throw std::runtime_error("foldattn: at most 160 keys on 2 waves");
-  switch (nit) {
-    MOCR_FA(1) MOCR_FA(2) MOCR_FA(3) MOCR_FA(4) MOCR_FA(5) MOCR_FA(6) MOCR_FA(7) MOCR_FA(8) MOCR_FA(9) MOCR_FA(10)
-    default: throw std::runtime_error("foldattn: at most 288 keys");
+  if ((nw == 2 && nit > 10) || (nw == 1 && nit > 5))
+    throw std::runtime_error("foldattn: at most 160 keys on 2 waves, 40 on 1");
+  if (nw == 4) {
+    switch (nit) {
+      MOCR_FA(1, 4) MOCR_FA(2, 4) MOCR_FA(3, 4) MOCR_FA(4, 4) MOCR_FA(5, 4) MOCR_FA(6, 4) MOCR_FA(7, 4) MOCR_FA(8, 4)
+      MOCR_FA(9, 4)
+      default: throw std::runtime_error("foldattn: at most 288 keys");
+    }
+  } else if (nw == 2) {
+    switch (nit) {
+      MOCR_FA(1, 2) MOCR_FA(2, 2) MOCR_FA(3, 2) MOCR_FA(4, 2) MOCR_FA(5, 2) MOCR_FA(6, 2) MOCR_FA(7, 2) MOCR_FA(8, 2)
+      MOCR_FA(9, 2) MOCR_FA(10, 2)
+      default: break;
+    }
+  } else {
+    switch (nit) {
+      MOCR_FA(1, 1) MOCR_FA(2, 1) MOCR_FA(3, 1) MOCR_FA(4, 1) MOCR_FA(5, 1)
+      default: break;
+    }
   }
 #undef MOCR_FA
 #undef MOCR_FA3

@@ -1,9 +1,9 @@
 #!/bin/bash
-# decode attention on 2 vs 4 waves per (row, head): phase clocks, parity, decode chain
+# decode attention: phase clocks (1 / 2 / 4 waves), parity, decode chain
 set -o pipefail
 O=gpurun_out/aw; mkdir -p $O
 for args in "cross 256 100" "self 256 16" "self 256 60" "self 256 120"; do
-  for w in 4 2; do timeout -k 10 60 ./tools/attn_ts $args $w | head -2 | tail -2 || exit 1; done
+  for w in ${WAVES:-0}; do timeout -k 10 60 ./tools/attn_ts $args $w | head -2 | tail -2 || exit 1; done
 done
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_full.py -m gpu -x -v -rP --timeout 300 --timeout-method thread \
   -k "teacher_forced or b256_chain or config2 or eos or invariance" > $O/tests.log 2>&1 || { echo "TESTS FAILED"; tail -40 $O/tests.log; exit 1; }
