@@ -282,6 +282,15 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
 #pragma unroll
       for (int mf = 0; mf < MF; ++mf) {
         floatx4 x = ra[s][h][mf];
+#ifdef MOCR_FOLD_NOXFORM  // timing probe: no LN / unfold transform, no split (wrong results)
+        {
+          const int lt = q + 16 * (h * 2 + (c >> 1));
+          char* f = a_s + mf * 2048 + lt * 16 + (c & 1) * 8;
+          *reinterpret_cast<uint2*>(f) = make_uint2(__float_as_uint(x[0]), __float_as_uint(x[1]));
+          *reinterpret_cast<uint2*>(f + 1024) = make_uint2(__float_as_uint(x[2]), __float_as_uint(x[3]));
+          continue;
+        }
+#endif
         if ((S1 && in1) || (S2 && !YT && !in1)) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -399,7 +408,7 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
           step(dpp<0x4E>(m), __builtin_amdgcn_mov_dpp(ix, 0x4E, 0xF, 0xF, false));
           step(dpp<0x141>(m), __builtin_amdgcn_mov_dpp(ix, 0x141, 0xF, 0xF, false));
           step(dpp<0x140>(m), __builtin_amdgcn_mov_dpp(ix, 0x140, 0xF, 0xF, false));
-          const float e = row_sum<16>(cv ? expf(v - m) : 0.f);
+          const float e = row_sum<16>(cv ? __expf(v - m) : 0.f);  // v_exp_f32
           if (ecol == 0 && orow < B)
             reinterpret_cast<floatx4*>(p.part)[(size_t)orow * (p.NZ / 16) + zc / 16] =
                 floatx4{m, __int_as_float(ix), e, 0.f};

@@ -13,8 +13,8 @@ namespace mocr {
 // running (max, first argmax, sum exp(l - max)) merge; ties go to the lower index
 __device__ __forceinline__ void sel_merge(float& b1, int& i1, float& s1, float b2, int i2, float s2) {
   const float m = fmaxf(b1, b2);
-  const float f1 = b1 == -INFINITY ? 0.f : expf(b1 - m);
-  const float f2 = b2 == -INFINITY ? 0.f : expf(b2 - m);
+  const float f1 = b1 == -INFINITY ? 0.f : __expf(b1 - m);
+  const float f2 = b2 == -INFINITY ? 0.f : __expf(b2 - m);
   s1 = s1 * f1 + s2 * f2;
   if (b2 > b1 || (b2 == b1 && i2 < i1)) i1 = i2;
   b1 = m;
