@@ -18,11 +18,12 @@ import json
 import sys
 
 
-def classes_in_order(mlp_fused=(), attn_fused=(), attn_noproj=()):
+def classes_in_order(mlp_fused=(), attn_fused=(), attn_noproj=(), lnqkv=(), lnmerge=()):
     """Encoder dispatch classes in launch order; stages in `mlp_fused` run norm2 + MLP as one
     kernel (mlp.hip) instead of layernorm, fc1, fc2, stages in `attn_fused` run norm1 +
     qkv + W-MSA + proj as one kernel (wattn.hip), stages in `attn_noproj` norm1 + qkv +
-    W-MSA as one kernel, then the proj GEMM."""
+    W-MSA as one kernel, then the proj GEMM; stages in `lnqkv` norm1 + qkv as one kernel
+    (mlp.hip lngemm384_kernel), merges in `lnmerge` gather + norm + reduction as one."""
     names = ["split(weights)", "split(kv-weights)", "stem"]
     depth = (2, 2, 6, 2)
     for s in range(4):
@@ -31,19 +32,23 @@ def classes_in_order(mlp_fused=(), attn_fused=(), attn_noproj=()):
                 names += [f"s{s+1}.attn"]
             elif s + 1 in attn_noproj:
                 names += [f"s{s+1}.attn", f"s{s+1}.proj"]
+            elif s + 1 in lnqkv:
+                names += [f"s{s+1}.lnqkv", f"s{s+1}.wattn", f"s{s+1}.proj"]
             else:
                 names += [f"s{s+1}.ln1", f"s{s+1}.qkv", f"s{s+1}.wattn", f"s{s+1}.proj"]
             names += [f"s{s+1}.mlp"] if s + 1 in mlp_fused else [f"s{s+1}.ln2", f"s{s+1}.fc1", f"s{s+1}.fc2"]
         if s < 3:
-            names += [f"merge{s+1}.ln", f"merge{s+1}"]
+            names += [f"merge{s+1}"] if s + 1 in lnmerge else [f"merge{s+1}.ln", f"merge{s+1}"]
     names += ["split(memory)", "memproj", "crosskv"]
     return names
 
 
 def with_memkv24(names, kn):
-    """bf16x3 engines append the fp24 split of the cross K/V (one dispatch per layer)."""
+    """bf16x3 engines append the fp24 split (one dispatch per layer) or the int16
+    quantisation (one dispatch) of the cross K/V unless the crosskv epilogue quantises."""
     n = sum("split_kv_fp24" in k for k in kn)
-    return names + ["memkv(fp24)"] * n
+    q = sum("quant_kv_i16" in k for k in kn)
+    return names + ["memkv(fp24)"] * n + ["memkv(i16)"] * q
 
 
 def main(fetch_csv, write_csv, out, decode_steps=0):
@@ -58,7 +63,10 @@ def main(fetch_csv, write_csv, out, decode_steps=0):
                    ({3} if any("mlp384_kernel" in k for k in kn) else set()))
     afused = sorted({1 if "swin_attn_kernel<96" in k else 2 for k in kn if "swin_attn_kernel" in k})
     anoproj = [3] if any("swin_attn_noproj_kernel" in k for k in kn) else []
-    names = with_memkv24(classes_in_order(fused, afused, anoproj), kn)
+    n_lng = sum("lngemm384_kernel" in k for k in kn)  # 6 stage-3 blocks and / or merge 1
+    lnqkv = [3] if n_lng >= 6 else []
+    lnmerge = [1] if n_lng in (1, 7) else []
+    names = with_memkv24(classes_in_order(fused, afused, anoproj, lnqkv, lnmerge), kn)
     # load-time bf16 splits before the stem: weights, kv-weights, and (bf16x3) the folded
     # decoder weights; fp32 mode has none
     n_split = next(i for i, k in enumerate(kn) if "stem" in k)
