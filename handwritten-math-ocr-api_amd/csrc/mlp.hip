@@ -869,8 +869,11 @@ __global__ void __launch_bounds__(256) lngemm384_kernel(LnGemm384Params p) {
 #pragma unroll
     for (int tt = 0; tt < TT; ++tt) {
       float* o = p.out + orow[tt] + col;
-      __builtin_nontemporal_store(acc[0][tt] + bb0, reinterpret_cast<floatx4*>(o));
-      __builtin_nontemporal_store(acc[1][tt] + bb1, reinterpret_cast<floatx4*>(o + 4));
+      // plain stores: the two 16-B halves of a lane's 32 B leave in two instructions, and
+      // L2 merges them into whole lines (non-temporal stores wrote each 64-B segment twice:
+      // WRITE_SIZE 1365 vs 680 MB per launch at B = 256)
+      *reinterpret_cast<floatx4*>(o) = acc[0][tt] + bb0;
+      *reinterpret_cast<floatx4*>(o + 4) = acc[1][tt] + bb1;
     }
     // W(jc + 1) landed: in issue order W(jc + 2) and stores(jc) may be outstanding behind
     // it (and stores(jc - 1) is waited for: a per-chunk count that differs in chunk 0 makes
