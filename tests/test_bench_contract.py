@@ -70,7 +70,7 @@ def test_e2e_roofline_is_baseline_md_section4(bench):
 
 
 def test_committed_pmc_traffic_covers_the_roofline_classes(bench):
-    for cls in ("s3.mlp", "s1.attn", "s3.qkv", "decode.step"):  # the bench's roofline classes at B = 256
+    for cls in ("s3.mlp", "s1.attn", "s3.lnqkv", "decode.step"):  # the bench's roofline classes at B = 256
         t = bench.pmc_traffic("bf16x3", cls)
         assert t is not None and t > 0, cls
     assert bench.pmc_traffic("bf16x3", "no.such.class") is None
