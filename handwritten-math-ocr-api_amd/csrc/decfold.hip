@@ -294,7 +294,7 @@ __device__ unsigned long long g_attn_ts[8192 * 8];
 // KVF: K/V (and the self-attention cache) in fp32 (0) or fp24 planes (1, common.h); 2:
 // cross-attention K/V in int16 with per-column scales (the scales of K fold into q, those
 // of V into the output).
-// NW waves (8 key rows each per pass; the selection needs all 4 of its 256 threads).
+// NW waves (8 key rows each per pass; the selection runs on all 64 NW threads).
 template <bool SELF, bool ZS, bool SEL, int NIT, int KVF, int NW>
 __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   MOCR_ATS(0, __builtin_amdgcn_s_memrealtime());
@@ -303,7 +303,6 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   constexpr int RPW = 8;  // key rows per wave instruction
   constexpr bool F24 = KVF == 1, I16 = KVF == 2;
   static_assert(!(SELF && I16), "int16 K/V: cross-attention only");
-  static_assert(!SEL || NW == 4, "the selection runs on 256 threads");
   __shared__ floatx4 po[NW][LPR];
   __shared__ float pm[NW], ps[NW];
 
@@ -342,7 +341,7 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   floatx4 zv[NP], sv[NP], cv[NP];
   if constexpr (SEL) {
     static_assert(SELF && !ZS, "selection runs in layer 0's self-attention");
-    const int tok = greedy_select(p.sel, b, h == 0);
+    const int tok = greedy_select<NW>(p.sel, b, h == 0);
     const int tk = max(tok, 0);  // -1: the batch stopped before step t-1 (nothing is written)
     const float* qt = p.qtab + (size_t)tk * 3 * kD + cc;
     const float* qp = p.qpos + (size_t)t * 3 * kD + cc;
@@ -548,25 +547,23 @@ void launch_dec_foldattn(const FoldAttnParams& p, bool self_attn, hipStream_t s)
   if (i16 && (self_attn || f24 || !p.V16 || !p.Ks || !p.Vs || p.s_b < kD))
     throw std::runtime_error("foldattn: int16 K/V is cross-attention only, with K, V and their scales");
   if (p.B <= 0) return;
-  // waves per workgroup: 2 unless the selection runs here (it needs 256 threads) or the
-  // keys exceed 2 x 8 x 10 (tools/attn_ts: the 4-wave kernel's per-wave fixed work --
-  // statistics, unfold, the reductions -- made 8 waves per SIMD VALU-bound: cross 9.9 ->
-  // 8.5 us, self at t = 16 6.9 -> 5.4, t = 120 10.8 -> 10.3)
+  // waves per workgroup: 2 unless the keys exceed 2 x 8 x 10 (tools/attn_ts: the 4-wave
+  // kernel's per-wave fixed work -- statistics, unfold, the reductions -- made 8 waves per
+  // SIMD VALU-bound: cross 9.9 -> 8.5 us, self at t = 16 6.9 -> 5.4, t = 120 10.8 -> 10.3)
 #ifndef MOCR_ATTN_WAVES
 #define MOCR_ATTN_WAVES 2
 #endif
   // (one wave up to 40 keys: self-attention at t = 16 5.42 -> 4.75 us; equal at t = 60,
   // slower from there and for the 144 memory keys, 8.5 -> 9.3 us)
-  const int nw = p.waves ? p.waves : ((p.sel_on || p.n > 160) ? 4 : (p.n <= 40 ? 1 : MOCR_ATTN_WAVES));
+  const int nw = p.waves ? p.waves : (p.n > 160 ? 4 : (p.n <= 40 ? 1 : MOCR_ATTN_WAVES));
   if (nw != 1 && nw != 2 && nw != 4) throw std::runtime_error("foldattn: 1, 2 or 4 waves");
-  if (p.sel_on && nw != 4) throw std::runtime_error("foldattn: the selection needs 4 waves");
   const int nit = (p.n + 8 * nw - 1) / (8 * nw);  // 8 nw key rows per workgroup pass
   const dim3 grid(p.B, kD / 32);
 #define MOCR_FA2(N, F, W)                                                                  \
   if (self_attn && zs)                                                                     \
     dec_foldattn_kernel<true, true, false, N, F, W><<<grid, 64 * W, 0, s>>>(p);           \
   else if (self_attn && p.sel_on)                                                          \
-    dec_foldattn_kernel<true, false, true, N, F, 4><<<grid, 256, 0, s>>>(p);              \
+    dec_foldattn_kernel<true, false, true, N, F, W><<<grid, 64 * W, 0, s>>>(p);           \
   else if (self_attn)                                                                      \
     dec_foldattn_kernel<true, false, false, N, F, W><<<grid, 64 * W, 0, s>>>(p);          \
   else if (zs)                                                                             \

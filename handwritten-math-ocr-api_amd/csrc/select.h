@@ -20,11 +20,14 @@ __device__ __forceinline__ void sel_merge(float& b1, int& i1, float& s1, float b
   b1 = m;
 }
 
-// Row b of step a.t, all 256 threads of the workgroup.  Returns the token fed to step t+1
+// Row b of step a.t, all 64 W threads of the workgroup.  Returns the token fed to step t+1
 // (workgroup-uniform; the forced token when teacher forcing), or -1 when the batch stopped
 // before step t.  `bookkeep`: this workgroup writes ids / feed / logp / the finished flags
 // and the stop state (one workgroup per row may).
+template <int W = 4>
 __device__ __forceinline__ int greedy_select(const SelectArgs& a, int b, bool bookkeep) {
+  constexpr int NT = 64 * W;
+  constexpr int NP = (512 + NT - 1) / NT;  // partials per thread (nparts <= 512)
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int t = a.t;
@@ -33,30 +36,30 @@ __device__ __forceinline__ int greedy_select(const SelectArgs& a, int b, bool bo
   float best = -INFINITY, sum = 0.f;
   int bidx = 0x7fffffff;
   constexpr int CH = 20;  // loads in flight per thread: one round for V <= 5120
-  if (a.part) {  // per-16-column-tile partials of the logits kernel: 2 per thread for V <= 8192
+  if (a.part) {  // per-16-column-tile partials of the logits kernel (nparts <= 512)
     const floatx4* P = reinterpret_cast<const floatx4*>(a.part) + (size_t)b * a.nparts;
-    floatx4 q[2];
+    floatx4 q[NP];
 #pragma unroll
-    for (int c = 0; c < 2; ++c) q[c] = P[min(tid + 256 * c, a.nparts - 1)];
+    for (int c = 0; c < NP; ++c) q[c] = P[min(tid + NT * c, a.nparts - 1)];
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
-      if (tid + 256 * c < a.nparts) sel_merge(best, bidx, sum, q[c][0], __float_as_int(q[c][1]), q[c][2]);
+    for (int c = 0; c < NP; ++c)
+      if (tid + NT * c < a.nparts) sel_merge(best, bidx, sum, q[c][0], __float_as_int(q[c][1]), q[c][2]);
   }
-  for (int j0 = a.part ? V : tid; j0 < V; j0 += 256 * CH) {
+  for (int j0 = a.part ? V : tid; j0 < V; j0 += NT * CH) {
     float vals[CH];
     // unpredicated loads (a clamped column), masked after: a predicated load per element
     // becomes a branch + vmcnt(0) each
 #pragma unroll
-    for (int c = 0; c < CH; ++c) vals[c] = L[min(j0 + 256 * c, V - 1)];
+    for (int c = 0; c < CH; ++c) vals[c] = L[min(j0 + NT * c, V - 1)];
 #pragma unroll
-    for (int c = 0; c < CH; ++c) vals[c] = (j0 + 256 * c < V) ? vals[c] : -INFINITY;
+    for (int c = 0; c < CH; ++c) vals[c] = (j0 + NT * c < V) ? vals[c] : -INFINITY;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const float v = vals[c];
       if (v > best) {
         sum = sum * expf(best - v) + 1.0f;
         best = v;
-        bidx = j0 + 256 * c;
+        bidx = j0 + NT * c;
       } else if (v != -INFINITY) {
         sum += expf(v - best);
       }
@@ -69,8 +72,8 @@ __device__ __forceinline__ int greedy_select(const SelectArgs& a, int b, bool bo
     const float os = __shfl_xor(sum, o, 64);
     sel_merge(best, bidx, sum, ob, oi, os);
   }
-  __shared__ float sv[4], ss[4];
-  __shared__ int si_[4];
+  __shared__ float sv[W], ss[W];
+  __shared__ int si_[W];
   __shared__ int s_next;
   if ((tid & 63) == 0) {
     sv[wave] = best;
@@ -82,7 +85,7 @@ __device__ __forceinline__ int greedy_select(const SelectArgs& a, int b, bool bo
   bidx = si_[0];
   sum = ss[0];
 #pragma unroll
-  for (int w = 1; w < 4; ++w) sel_merge(best, bidx, sum, sv[w], si_[w], ss[w]);
+  for (int w = 1; w < W; ++w) sel_merge(best, bidx, sum, sv[w], si_[w], ss[w]);
   DecodeState* st = a.st;
   if (dec_skip(a.stop_batch ? st : nullptr, t)) return -1;
   // A row without a finite maximum (NaN logits never win `v > best`) would leave bidx at
