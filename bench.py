@@ -10,8 +10,9 @@ then, with N > 1 ranks, an RCCL all-gather of the decoded token streams inside
 libmathocr.so (``mocr_group_gather_ids``; image-parallel shards, no other collective;
 torch.distributed over gloo carries only the group id, barriers and the timing max).
 
-Each engine call takes G = --chain-batches batches of 64 (default 4): one encode of the
-G*64 images and ONE decode chain of G*64 rows.  A greedy step is a chain of 41 dependent
+Each engine call takes G = --chain-batches batches of 64 (default: 4, or 5 when that makes
+the timed batches a whole number of calls per replica, see ``auto_chain``): one encode of
+the G*64 images and ONE decode chain of G*64 rows.  A greedy step is a chain of 41 dependent
 kernels whose launch and memory latencies do not grow with the rows, so G batches in one
 chain amortise them G ways (profiles/r03/decode_chain_probe_*.log); rows are
 independent (stop="none" here; tests/test_gpu_parity.py::test_wide_chain_rows_bitwise
@@ -19,6 +20,13 @@ holds a row's logits bitwise equal between a 2-row and a 160-row chain).  Each G
 pipelines calls through R engine replicas (``pipeline.ReplicaPool``, one host thread and
 one HIP stream each), so one call's decode overlaps the next call's encoder.  Rank 0
 prints one JSON line; ``value`` = all images all ranks processed / max-over-ranks time.
+
+``--gpus N`` (N > 1) without a launcher (no WORLD_SIZE in the environment) starts
+``torch.distributed.run --nproc-per-node N`` on this file as a child process, before
+anything touches the GPU, and exits with its status; under a launcher, --gpus must equal
+WORLD_SIZE.  The line's ``rccl_ranks`` is what RCCL's communicator counts
+(``mocr_group_size`` = ncclCommCount), null when the ranks share one device and gather
+over the host group.
 """
 from __future__ import annotations
 
@@ -26,7 +34,9 @@ import argparse
 import importlib
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -49,7 +59,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=64,
                     help="timed batches per GPU (the replica pipeline's fill and drain are inside the timed "
                          "region: 64 batches read 0.8 %% above 24, profiles/r02/bench_steps_probe.log)")
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--batch", type=int, default=64, help="images per batch (per GPU)")
     ap.add_argument("--image", type=int, nargs=2, default=[384, 384])
     ap.add_argument("--tokens", type=int, default=128)
@@ -57,8 +67,10 @@ def parse():
     ap.add_argument("--replicas", type=int, default=None,
                     help="engine replicas pipelining calls per GPU (default: 2 with 4-batch chains, 4 with 1)")
     ap.add_argument("--chain-batches", dest="chain", type=int, default=None,
-                    help="64-image batches per engine call / decode chain (default 4; 1 for res18trans, whose "
-                         "encoder attends across its batch, and for beam search)")
+                    help="64-image batches per engine call / decode chain (default: auto_chain, 4 or 5; 1 for "
+                         "res18trans, whose encoder attends across its batch, and for beam search)")
+    ap.add_argument("--no-secondary", dest="secondary", action="store_false", default=True,
+                    help="skip the literal config-2 pass (64 images per engine call, 4 replicas)")
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     ap.add_argument("--cpu-sample", type=int, default=64,
@@ -73,13 +85,56 @@ def parse():
     a = ap.parse_args()
     if a.beam and a.arch != "swin":
         ap.error("--beam is measured on the Swin path")
-    if a.chain is None:
-        a.chain = 1 if (a.arch != "swin" or a.beam) else 4
-    if a.chain > 1 and (a.arch != "swin" or a.beam):
+    if a.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if a.chain is not None and a.chain > 1 and (a.arch != "swin" or a.beam):
         ap.error("--chain-batches > 1 is for the Swin greedy path (the ResNet18-trans encoder attends across its batch)")
     if a.replicas is None:
-        a.replicas = 2 if a.chain > 1 else 4
+        a.replicas = 2 if (a.chain is None or a.chain > 1) and a.arch == "swin" and not a.beam else 4
+    if a.chain is None:
+        a.chain = 1 if (a.arch != "swin" or a.beam) else auto_chain(a.steps, a.replicas)
     return a
+
+
+def auto_chain(steps, replicas):
+    """Batches per engine call: 4 (256-row decode chains), or 5 when 4 would leave the
+    timed calls uneven over the replicas and 5 does not.  An uneven count leaves the last
+    call's decode chain running alone at the end of the timed region (one 256-row chain
+    alone runs at ~60 % of two concurrent ones): --steps 20 is 5 calls of 4
+    (one replica runs 3) but 4 calls of 5 (2 each)."""
+    for g in (4, 5):
+        if steps % g == 0 and (steps // g) % replicas == 0:
+            return g
+    return 4
+
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(n, argv, port):
+    """The torch.distributed.run command that runs this file on n local ranks."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def launch_if_needed(args, argv, env=None):
+    """--gpus N > 1 without a launcher: run N ranks under torch.distributed.run as a child
+    process (never exec: the parent has not touched the GPU, but the child must own it)
+    and return its exit status; None when this process is a rank (or N = 1).  Under a
+    launcher, WORLD_SIZE must equal --gpus."""
+    env = os.environ if env is None else env
+    world = env.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: pass --gpus equal to the "
+                             f"launcher's --nproc-per-node")
+        return None
+    if args.gpus == 1:
+        return None
+    return subprocess.run(launcher_cmd(args.gpus, argv, free_port())).returncode
 
 
 def cpu_threads():
@@ -205,6 +260,9 @@ def roofline_decode(stats, precision, rows, steps):
 
 def main():
     args = parse()
+    rc = launch_if_needed(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -215,6 +273,7 @@ def main():
     pkg = importlib.import_module("handwritten-math-ocr-api_amd")
     grp = None
     gather = "none"
+    rccl_ranks = None
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("gloo")  # host-side control only
@@ -225,6 +284,9 @@ def main():
         else:
             grp = pkg.parallel.RcclGroup(world, rank, local)  # RCCL inside libmathocr.so
             gather = "rccl (mocr_group_gather_ids)"
+            rccl_ranks = grp.size()  # ncclCommCount
+            if rccl_ranks != world:
+                raise SystemExit(f"RCCL communicator counts {rccl_ranks} ranks, WORLD_SIZE is {world}")
     H, W = args.image
     B, S, R, G = args.batch, args.tokens, args.replicas, args.chain
     BG = B * G  # images per engine call (one encode, one decode chain of BG rows)
@@ -249,7 +311,7 @@ def main():
 
     def step(eng, _k):
         t0 = time.perf_counter()
-        ids = torch.empty((BG, S + 1), dtype=torch.int32, device=dev)
+        ids = torch.empty((eng.batch, S + 1), dtype=torch.int32, device=dev)
         eng.encode()
         if args.beam:
             r = eng.beam_search(beam=args.beam, max_steps=S, stop="none")
@@ -258,7 +320,7 @@ def main():
             eng.decode_into(ids, max_steps=S, stop="none")
         return ids, time.perf_counter() - t0
 
-    def run(n):
+    def run(n, pool=pool):
         lat = []
         for ids, dt in pool.imap(step, range(n)):
             if grp:
@@ -311,6 +373,44 @@ def main():
         e1.close()
         iso = {"call_latency_ms": statistics.median(ts) * 1e3, "b1_latency_ms": statistics.median(t1s) * 1e3,
                "stats": stats}
+        # the host->device copy of one call's images, which the timed region leaves out (the
+        # images are resident in HBM): pageable numpy source, and pinned
+        host = pkg.synth.make_images(BG, H, W, seed0=1000)
+        pinned = torch.from_numpy(host).pin_memory()
+        h2d = {"pageable": [], "pinned": []}
+        for _ in range(3):
+            for kind, src in (("pageable", torch.from_numpy(host)), ("pinned", pinned)):
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                src.to(dev, non_blocking=kind == "pinned")
+                torch.cuda.synchronize()
+                h2d[kind].append(time.perf_counter() - t1)
+        iso["h2d_ms"] = {k: statistics.median(v) * 1e3 for k, v in h2d.items()}
+        iso["h2d_bytes"] = host.nbytes
+        del pinned
+
+    literal = None
+    if rank == 0 and world == 1 and args.secondary and G > 1:
+        # BASELINE config 2 read literally: 64 images per engine call (one 64-row chain), 4
+        # replicas, images resident; a shorter pass beside the headline
+        pool.close()
+        lit_pool = pkg.pipeline.ReplicaPool(4, **dict(ekw, max_batch=B))
+        lit_pool.load_weights(weights)
+        for i, e in enumerate(lit_pool.engines):
+            e.set_images(torch.from_numpy(pkg.synth.make_images(B, H, W, seed0=1000 + i * B)).to(dev))
+        lit_calls = 32
+        run(8, lit_pool)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        lit_lat = run(lit_calls, lit_pool)
+        torch.cuda.synchronize()
+        lit_s = time.perf_counter() - t1
+        lit_pool.close()
+        literal = {"value": B * lit_calls / lit_s, "unit": "images/sec", "batches": lit_calls,
+                   "images_per_call": B, "replicas": 4, "ms_per_step": lit_s / lit_calls * 1e3,
+                   "p50_call_latency_loaded_ms": statistics.median(lit_lat) * 1e3,
+                   "note": "64 images per engine call (one encode of 64, one 64-row decode chain), 4 replicas "
+                           "pipelining, 8 untimed warm-up calls"}
 
     if rank != 0:
         pool.close()
@@ -327,6 +427,7 @@ def main():
         "value": value,
         "unit": "images/sec",
         "n_gpus": world,
+        "rccl_ranks": rccl_ranks,
         "steps": steps,
         "warmup": wcalls * G,
         "ms_per_step": elapsed / steps * 1e3,
@@ -348,16 +449,25 @@ def main():
         "e2e_roofline": {"value": value / world, "unit": "images/sec per GPU", "peak": E2E_ROOFLINE_IMG_S,
                          "frac": value / world / E2E_ROOFLINE_IMG_S,
                          "basis": "BASELINE.md §4: 26.39 GFLOP/img at 2.5 PF + 245 MB/img bf16 decode traffic at 8 TB/s"},
-        # latency of a 64-image batch under the bench's load: it completes with its call
-        "p50_batch_latency_loaded_ms": statistics.median(lat) * 1e3,
+        # an image's latency under the bench's load is its engine call's: the call's G batches
+        # complete together
+        "p50_call_latency_loaded_ms": statistics.median(lat) * 1e3,
         "p50_image_latency_ms": statistics.median(lat) * 1e3,
-        "latency_note": (f"p50_image_latency_ms is the loaded latency of an image's call ({G} batch(es) of {B} "
-                         f"through encode + decode, {R} replicas pipelining); p50_image_latency_b1_ms is one image "
-                         f"alone (B=1)"),
+        "latency_note": (f"p50_image_latency_ms = p50_call_latency_loaded_ms: the loaded latency of an image's "
+                         f"engine call ({G} batch(es) of {B} through encode + decode, {R} replicas pipelining; "
+                         f"rounds 1-3 named it p50_batch_latency_loaded_ms); "
+                         f"p50_image_latency_b1_ms is one image alone (B=1)"),
     }
+    if literal:
+        out["config2_literal"] = literal
     if iso:
-        out["p50_batch_latency_unloaded_ms"] = iso["call_latency_ms"]
+        out["p50_call_latency_unloaded_ms"] = iso["call_latency_ms"]
         out["p50_image_latency_b1_ms"] = iso["b1_latency_ms"]
+        h2d = iso["h2d_ms"]["pageable"]
+        out["h2d_ms_per_call"] = iso["h2d_ms"]
+        out["h2d_note"] = (f"host->device copy of one call's {BG} images ({iso['h2d_bytes'] / 1e6:.0f} MB fp32), "
+                           f"outside the timed region; serialised with the calls it would give "
+                           f"{BG * calls / (elapsed + calls * h2d * 1e-3) * world:.0f} img/s (pageable source)")
         rd = roofline_decode(iso["stats"], args.precision, BG, S)
         rg = roofline(iso["stats"], dtype, args.precision)
         ra = roofline(iso["stats"], dtype, args.precision, attention=True)
@@ -384,7 +494,8 @@ def main():
                                  for k, v in sorted(iso["stats"].items())}
     if args.cpu_baseline and world == 1 and args.arch == "swin" and not args.beam:
         out["cpu_baseline"] = cpu_baseline(args, pkg)
-    pool.close()
+    if not literal:
+        pool.close()
     print(json.dumps(out))
     if grp:
         grp.close()

@@ -963,21 +963,26 @@ __global__ void __launch_bounds__(512) gemm_x3_stagq_kernel(GemmParams p) {
       for (int j = 0; j < WTN; ++j) {
         const int col = col0 + wc * EW + j * 16 + l16;
         const float bj = p.bias ? p.bias[col] : 0.f;
-        float m = 0.f;
+        float m = 0.f, nan = 0.f;
 #pragma unroll
         for (int i = 0; i < WTM; ++i)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             acc[i][j][r] += bj;
-            m = fmaxf(m, fabsf(acc[i][j][r]));
+            m = fmaxf(m, fabsf(acc[i][j][r]));  // fmaxf drops NaN operands: tracked apart
+            nan = acc[i][j][r] != acc[i][j][r] ? 1.f : nan;
           }
         m = fmaxf(m, __shfl_xor(m, 16, 64));
         m = fmaxf(m, __shfl_xor(m, 32, 64));
+        nan = fmaxf(nan, __shfl_xor(nan, 16, 64));
+        nan = fmaxf(nan, __shfl_xor(nan, 32, 64));
         const float inv = m > 0.f ? 32767.f / m : 0.f;
         if (kq == 0 && img_row < M) {
           const int blk = col / p.col_split;
+          // a NaN anywhere in the column makes its scale NaN, so it reaches the logits and the
+          // engine's non-finite check as on the fp32 / fp24 paths (inf gives an inf scale)
           p.kv16_scale[blk * p.kv16_sstride + (size_t)(img_row / p.kv_M) * p.col_split + (col - blk * p.col_split)] =
-              m > 0.f ? m / 32767.f : 1.f;
+              nan != 0.f ? __builtin_nanf("") : (m > 0.f ? m / 32767.f : 1.f);
         }
 #pragma unroll
         for (int i = 0; i < WTM; ++i)

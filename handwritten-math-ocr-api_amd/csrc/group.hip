@@ -27,6 +27,7 @@ struct Rccl {
   ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
   ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*comm_count)(const ncclComm_t, int*) = nullptr;
   ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
   const char* (*error_string)(ncclResult_t) = nullptr;
 };
@@ -46,6 +47,7 @@ const Rccl& rccl() {
     bind(x.h, x.get_unique_id, "ncclGetUniqueId");
     bind(x.h, x.comm_init_rank, "ncclCommInitRank");
     bind(x.h, x.comm_destroy, "ncclCommDestroy");
+    bind(x.h, x.comm_count, "ncclCommCount");
     bind(x.h, x.all_gather, "ncclAllGather");
     bind(x.h, x.error_string, "ncclGetErrorString");
     return x;
@@ -135,6 +137,16 @@ int mocr_group_destroy(mocr_group* g) {
   if (g->shapes_host) (void)hipHostFree(g->shapes_host);
   delete g;
   return 0;
+}
+
+int mocr_group_size(const mocr_group* g, int* ranks_out) {
+  try {
+    if (!g || !ranks_out) throw std::runtime_error("null argument");
+    check(rccl().comm_count(g->comm, ranks_out), "ncclCommCount");
+    return 0;
+  } catch (const std::exception& ex) {
+    return group_fail(ex);
+  }
 }
 
 int mocr_group_gather_ids(mocr_group* g, const int32_t* ids_dev, int rows, int width, int32_t* ids_all_dev,

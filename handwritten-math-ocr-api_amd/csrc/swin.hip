@@ -598,21 +598,28 @@ __global__ void __launch_bounds__(256) quant_kv_i16_kernel(const float* __restri
   const int c = threadIdx.x * 2;
   const float* src = kv + blockIdx.y * layer_stride + (size_t)b * M * 512 + c;
   float a0 = 0.f, a1 = 0.f;
+  bool n0 = false, n1 = false;  // fmaxf drops NaN operands: tracked apart
 #pragma unroll 8
   for (int m = 0; m < M; ++m) {
     const float2 v = *reinterpret_cast<const float2*>(src + (size_t)m * 512);
     a0 = fmaxf(a0, fabsf(v.x));
     a1 = fmaxf(a1, fabsf(v.y));
+    n0 |= v.x != v.x;
+    n1 |= v.y != v.y;
   }
   const float i0 = a0 > 0.f ? 32767.f / a0 : 0.f, i1 = a1 > 0.f ? 32767.f / a1 : 0.f;
+  // a NaN in a column makes its scale NaN (it reaches the logits and the engine's non-finite
+  // check, as on the fp32 / fp24 paths); an inf gives an inf scale
   *reinterpret_cast<float2*>(scale + blockIdx.y * scale_stride + (size_t)b * 512 + c) =
-      float2{a0 > 0.f ? a0 / 32767.f : 1.f, a1 > 0.f ? a1 / 32767.f : 1.f};
+      float2{n0 ? __builtin_nanf("") : (a0 > 0.f ? a0 / 32767.f : 1.f),
+             n1 ? __builtin_nanf("") : (a1 > 0.f ? a1 / 32767.f : 1.f)};
   int16_t* dst = q + blockIdx.y * layer_stride + ((size_t)(b * 2 + (c >> 8)) * 8 + ((c >> 5) & 7)) * M * 32 + (c & 31);
 #pragma unroll 8
   for (int m = 0; m < M; ++m) {
     const float2 v = *reinterpret_cast<const float2*>(src + (size_t)m * 512);
-    const int r0 = max(-32767, min(32767, (int)rintf(v.x * i0)));
-    const int r1 = max(-32767, min(32767, (int)rintf(v.y * i1)));
+    // clamp in float first: (int) of a NaN or out-of-range float is undefined
+    const int r0 = (int)rintf(fminf(fmaxf(v.x * i0, -32767.f), 32767.f));
+    const int r1 = (int)rintf(fminf(fmaxf(v.y * i1, -32767.f), 32767.f));
     *reinterpret_cast<uint32_t*>(dst + (size_t)m * 32) = ((uint32_t)r0 & 0xffffu) | ((uint32_t)r1 << 16);
   }
 }

@@ -23,7 +23,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libmathocr.so")
 PRECISION = {"fp32": 0, "bf16": 1, "bf16x3": 2}
 STOP = {"batch": 0, "none": 1}
 ARCH = {"swin": 0, "res18trans": 1}
-ABI_VERSION = 5
+ABI_VERSION = 6
 # kernel-path variants (include/mathocr.h MOCR_VARIANT_*): 0 = production
 VARIANT = {"unfused_attn": 1, "unfused_mlp": 2, "dec_unfolded": 4, "s4_fused_attn": 8, "window_rows": 16, "dec_narrow": 32,
            "logits_f32": 64, "s3_large_batch": 128, "kv_f32": 256,
@@ -89,6 +89,7 @@ def load_library(path: str = LIB_PATH):
         "mocr_group_destroy": (I, [P]),
         "mocr_group_last_error": (ctypes.c_char_p, []),
         "mocr_group_gather_ids": (I, [P, P, I, I, P, P]),
+        "mocr_group_size": (I, [P, ctypes.POINTER(ctypes.c_int)]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -122,7 +123,7 @@ def exported_symbols():
             "mocr_last_error", "mocr_load_weights", "mocr_set_images", "mocr_set_images_device", "mocr_encode",
             "mocr_get_memory", "mocr_decode", "mocr_decode_device", "mocr_decode_beam", "mocr_debug_encode_until",
             "mocr_set_timing", "mocr_get_timing", "mocr_set_encoder_pos", "mocr_set_cu_mask", "mocr_set_stream_priority", "mocr_group_unique_id", "mocr_group_create",
-            "mocr_group_destroy", "mocr_group_last_error", "mocr_group_gather_ids"]
+            "mocr_group_destroy", "mocr_group_last_error", "mocr_group_gather_ids", "mocr_group_size"]
 
 
 def make_config(img_hw=(96, 320), vocab=synth.VOCAB, max_batch=64, precision="fp32", n_layers=synth.N_LAYERS,

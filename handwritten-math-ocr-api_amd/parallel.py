@@ -61,6 +61,15 @@ class RcclGroup:
             raise MocrError(f"mocr_group_unique_id failed ({rc}): {lib.mocr_group_last_error().decode()}")
         return buf.raw
 
+    def size(self) -> int:
+        """Ranks RCCL's communicator counts (ncclCommCount via mocr_group_size)."""
+        from .engine import MocrError
+        n = ctypes.c_int(0)
+        rc = self.lib.mocr_group_size(self._h, ctypes.byref(n))
+        if rc != 0:
+            raise MocrError(f"mocr_group_size failed ({rc}): {self.lib.mocr_group_last_error().decode()}")
+        return n.value
+
     def gather_ids(self, ids_local, out=None):
         """All-gather a [rows, width] int32 CUDA tensor from every rank into [world*rows,
         width] (rank order), on the device; returns ``out``."""

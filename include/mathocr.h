@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MOCR_ABI_VERSION 5
+#define MOCR_ABI_VERSION 6
 
 /* Arithmetic of the engine. */
 enum {
@@ -240,6 +240,10 @@ int mocr_group_create(const uint8_t* id /* [MOCR_GROUP_ID_BYTES] */, int world, 
                       mocr_group** out);
 int mocr_group_destroy(mocr_group* g);
 const char* mocr_group_last_error(void);
+
+/* Ranks in the group as RCCL's communicator counts them (ncclCommCount): bench.py records
+ * it beside n_gpus ("rccl_ranks"), so the record shows RCCL saw every rank. */
+int mocr_group_size(const mocr_group* g, int* ranks_out);
 
 /* Collective: every rank passes its shard's ids [rows, width] int32 (device memory, e.g.
  * the ids mocr_decode_device wrote); ids_all_dev [world*rows, width] receives all shards

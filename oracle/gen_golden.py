@@ -77,6 +77,18 @@ def apply_eos_boost(weights, boost):
     return weights
 
 
+def apply_proj_outliers(weights, outliers):
+    """Scale rows of ``encoder.projection.weight`` (memory channels) by the given factors:
+    a badly conditioned encoder memory with outlier channels.
+    ``outliers``: list of [row, scale] pairs, or None."""
+    if outliers:
+        pw = weights["encoder.projection.weight"].copy()
+        for row, scale in outliers:
+            pw[int(row)] *= np.float32(scale)
+        weights["encoder.projection.weight"] = pw
+    return weights
+
+
 # ---------------------------------------------------------------------------------------------
 # Child process: reference glue (one process per reference tree, module names collide).
 # ---------------------------------------------------------------------------------------------
@@ -87,9 +99,10 @@ spec = json.loads(sys.argv[1])
 sys.path.insert(0, spec["stub"]); sys.path.insert(0, spec["src"]); sys.path.insert(0, spec["repo"])
 os.makedirs(spec["cwd"], exist_ok=True); os.chdir(spec["cwd"])
 pkg = importlib.import_module("handwritten-math-ocr-api_amd")
-from oracle.gen_golden import apply_eos_boost
+from oracle.gen_golden import apply_eos_boost, apply_proj_outliers
 arch = "res18trans" if spec["mode"] == "res18" else "swin"
 w = apply_eos_boost(pkg.synth.make_weights(spec["seed"], spec["variant"], arch=arch), spec["eos_boost"])
+w = apply_proj_outliers(w, spec.get("proj_outliers"))
 imgs = torch.from_numpy(pkg.synth.make_images(spec["B"], spec["H"], spec["W"], spec["img_seed"], spec["img_kind"]))
 vocab, idx2char = pkg.synth.synthetic_vocab(w["decoder.fc_out.weight"].shape[0])
 import config as cfgmod
@@ -209,10 +222,10 @@ def make_res18_fixture(name, *, seed, variant, eos_boost, B, H, W, pos_seed, ste
 
 
 def make_batch_fixture(name, *, seed, variant, eos_boost, B, H, W, img_seed=1000, img_kind="uniform",
-                       steps, stop, n_logit_steps, stub, n_mem=2, n_logit_rows=None):
+                       steps, stop, n_logit_steps, stub, n_mem=2, n_logit_rows=None, proj_outliers=None):
     pkg = _pkg()
     from oracle import model_ref
-    w = apply_eos_boost(pkg.synth.make_weights(seed, variant), eos_boost)
+    w = apply_proj_outliers(apply_eos_boost(pkg.synth.make_weights(seed, variant), eos_boost), proj_outliers)
     imgs = pkg.synth.make_images(B, H, W, img_seed, img_kind)
     vocab, idx2char = pkg.synth.synthetic_vocab(w["decoder.fc_out.weight"].shape[0])
     model = model_ref.build_model(w)
@@ -224,7 +237,7 @@ def make_batch_fixture(name, *, seed, variant, eos_boost, B, H, W, img_seed=1000
     glue = None
     if stop == "batch":
         glue = run_reference("batch", seed=seed, variant=variant, eos_boost=eos_boost, B=B, H=H, W=W,
-                             img_seed=img_seed, img_kind=img_kind, steps=steps, stub=stub)
+                             img_seed=img_seed, img_kind=img_kind, steps=steps, stub=stub, proj_outliers=proj_outliers)
         ref_ids = np.asarray(glue["ids"])
         assert np.array_equal(ref_ids, ys[:, 1:].numpy()), f"{name}: oracle ids differ from reference glue"
         assert np.array_equal(glue["logits"], logits), f"{name}: oracle logits differ from reference glue"
@@ -235,7 +248,7 @@ def make_batch_fixture(name, *, seed, variant, eos_boost, B, H, W, img_seed=1000
         os.path.join(GOLDEN, name + ".npz"),
         meta=json.dumps(dict(seed=seed, variant=variant, eos_boost=eos_boost, B=B, H=H, W=W, img_seed=img_seed,
                              img_kind=img_kind, steps=steps, stop=stop, glue_checked=glue is not None,
-                             strings=strings)),
+                             strings=strings, proj_outliers=proj_outliers)),
         ids=ys.numpy().astype(np.int32),
         logits=logits[:(n_logit_rows or n_mem), :n_logit_steps].astype(np.float32),
         margins=margins,
@@ -297,6 +310,13 @@ def main(only=None):
                            W=320, img_kind="ink", pos_seed=6, steps=150, stub=stub)
     if only == "res18":
         return
+    if only == "outlier":
+        # badly conditioned memory: config-2 shape, 4 memory channels
+        # scaled 30-100x, for the int16 cross-attention K/V (one scale per column over 144 keys)
+        make_batch_fixture("g384_b8_outlier", seed=1234, variant="init", eos_boost=0.0, B=8, H=384, W=384,
+                           steps=128, stop="batch", n_logit_steps=8, n_logit_rows=8, n_mem=8, stub=stub,
+                           proj_outliers=OUTLIER_ROWS)
+        return
     if only == "bench_c2":
         # config 2 only, teacher-forced logits of 8 rows x 8 steps (VERDICT r02 "Next" 4)
         make_batch_fixture("g384_b64_bench", seed=1234, variant="init", eos_boost=0.0, B=64, H=384, W=384,
@@ -331,6 +351,7 @@ def main(only=None):
 
 
 EOS_BOOST_R18 = 1.6
+OUTLIER_ROWS = [[3, 30.0], [77, 60.0], [141, 100.0], [200, -80.0]]
 
 if __name__ == "__main__":
     main(sys.argv[1] if len(sys.argv) > 1 else None)

@@ -79,9 +79,50 @@ def test_committed_pmc_traffic_covers_the_roofline_classes(bench):
 def test_default_run_is_one_gpu_minutes_scale(bench, monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py"])
     a = bench.parse()
-    assert a.gpus == 1 and a.steps == 64 and a.warmup == 3 and a.batch == 64 and a.tokens == 128
+    assert a.gpus == 1 and a.steps == 64 and a.warmup == 4 and a.batch == 64 and a.tokens == 128
     assert a.chain == 4 and a.replicas == 2 and a.precision == "bf16x3" and a.image == [384, 384]
     assert a.cpu_sample == 64 and a.cpu_runs == 3  # B = 64, median of 3
     monkeypatch.setattr(sys, "argv", ["bench.py", "--arch", "res18trans"])
     a = bench.parse()
     assert a.chain == 1 and a.replicas == 4  # its encoder attends across its batch of 64
+
+
+def test_auto_chain_keeps_timed_calls_even_over_replicas(bench, monkeypatch):
+    # the driver's --steps 20: 5 calls of 4 batches would leave one replica a third call
+    # whose decode chain runs alone; 4 calls of 5 give each replica 2
+    assert bench.auto_chain(20, 2) == 5 and bench.auto_chain(64, 2) == 4 and bench.auto_chain(8, 2) == 4
+    assert bench.auto_chain(7, 2) == 4
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--steps", "20", "--warmup", "5"])
+    a = bench.parse()
+    assert (a.chain, a.replicas) == (5, 2)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--steps", "20", "--chain-batches", "4"])
+    assert bench.parse().chain == 4
+
+
+def test_gpus_without_launcher_starts_torchrun_child(bench, monkeypatch):
+    """--gpus N > 1 with no WORLD_SIZE: bench.py runs N ranks under torch.distributed.run
+    as a child process (not exec) and returns its exit status."""
+    seen = {}
+
+    class Done:
+        returncode = 7
+
+    def fake_run(cmd, *a, **k):
+        seen["cmd"] = cmd
+        return Done()
+
+    monkeypatch.setattr(bench.subprocess, "run", fake_run)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "8", "--warmup", "4"])
+    a = bench.parse()
+    rc = bench.launch_if_needed(a, ["--gpus", "2", "--steps", "8", "--warmup", "4"], env={})
+    assert rc == 7
+    cmd = seen["cmd"]
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=2" in cmd and "--master-addr=127.0.0.1" in cmd and "--nnodes=1" in cmd
+    assert cmd[-7:] == [os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "8", "--warmup", "4"]
+    # one GPU, or a rank under a launcher: no child
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    assert bench.launch_if_needed(bench.parse(), [], env={}) is None
+    assert bench.launch_if_needed(a, [], env={"WORLD_SIZE": "2"}) is None
+    with pytest.raises(SystemExit):
+        bench.launch_if_needed(a, [], env={"WORLD_SIZE": "4"})

@@ -1,0 +1,81 @@
+"""GPU: the narrow K/V storage of the bench path on inputs it could get wrong.
+
+* A badly conditioned encoder memory: the config-2 shape (384x384,
+  greedy 128 steps, bench weights) with four memory channels scaled 30-100x
+  (``encoder.projection.weight`` rows, ``oracle/gen_golden.py`` OUTLIER_ROWS), fixture
+  pinned by the reference's own ``src/inference.py`` glue.  The int16 cross-attention K/V
+  keeps one scale per (layer, row, column) over the 144 keys, so large columns are where
+  it would lose bits.  Token ids exact, teacher-forced logits within 1e-3, on the
+  production path (quantised in the crosskv GEMM's epilogue), on a beam-capable engine
+  (quantised by ``quant_kv_i16_kernel``) and on the fp24 / fp32 K/V variants.
+* Non-finite values: a NaN in the memory must reach the engine's
+  non-finite-logits error on every K/V format, not decode into a finite wrong formula.
+"""
+import json
+
+import numpy as np
+import pytest
+
+from oracle.gen_golden import apply_proj_outliers
+
+pytestmark = pytest.mark.gpu
+
+LOGIT_TOL = 1e-3
+
+
+def outlier_engine(pkg, g, variant=(), max_beam=0):
+    m = g["meta"]
+    eng = pkg.Engine(img_hw=(m["H"], m["W"]), max_batch=m["B"], precision="bf16x3", variant=variant,
+                     max_beam=max_beam)
+    eng.load_weights(apply_proj_outliers(pkg.synth.make_weights(m["seed"], m["variant"]), m["proj_outliers"]))
+    eng.encode(pkg.synth.make_images(m["B"], m["H"], m["W"], seed0=m["img_seed"]))
+    return eng
+
+
+@pytest.mark.parametrize("variant,max_beam", [((), 0), ((), 2), (("cross_kv_f24",), 0), (("kv_f32",), 0)],
+                         ids=["int16-epilogue", "int16-pass", "fp24", "fp32"])
+def test_outlier_memory_kv_formats(pkg, golden, variant, max_beam):
+    g = golden("g384_b8_outlier")
+    m = g["meta"]
+    assert m["proj_outliers"] and m["glue_checked"]
+    eng = outlier_engine(pkg, g, variant, max_beam)
+    mem = eng.memory()
+    assert np.abs(g["memory"]).max() > 100.0  # the outlier channels are there
+    rel = float(np.abs(mem - g["memory"]).max() / np.abs(g["memory"]).max())
+    assert rel < 1e-4, rel
+    res = eng.decode(max_steps=m["steps"], stop="batch")
+    margins = g["margins"]
+    tie = 1e-4
+    for r in range(g["ids"].shape[0]):
+        near = np.flatnonzero(margins[r] < tie)
+        end = g["ids"].shape[1] if near.size == 0 else int(near[0]) + 1
+        np.testing.assert_array_equal(res.ids[r, :end], g["ids"][r, :end], err_msg=f"row {r}")
+    tf = eng.decode(max_steps=m["steps"], stop="none", forced=g["ids"], want_logits=True)
+    r, n = g["logits"].shape[:2]
+    err = float(np.abs(tf.logits[:r, :n] - g["logits"]).max())
+    ok = margins >= tie
+    np.testing.assert_array_equal(tf.logits.argmax(-1)[ok], g["ids"][:, 1:][ok])
+    print("PARITY_RECORD", json.dumps({"fixture": "g384_b8_outlier", "kv": list(variant) or ["int16"],
+                                       "max_beam": max_beam, "memory_rel_err": rel, "logits_max_abs_err": err,
+                                       "rows_equal": int(sum(np.array_equal(res.ids[i], g["ids"][i])
+                                                             for i in range(g["ids"].shape[0])))}))
+    assert err < LOGIT_TOL, err
+    eng.close()
+
+
+@pytest.mark.parametrize("variant,max_beam", [((), 0), ((), 2), (("cross_kv_f24",), 0), (("kv_f32",), 0)],
+                         ids=["int16-epilogue", "int16-pass", "fp24", "fp32"])
+def test_nan_memory_is_reported(pkg, variant, max_beam):
+    """One NaN in a memory channel's projection weight makes every cross-attention K/V
+    column NaN; the decode must fail with the non-finite-logits error."""
+    w = pkg.synth.make_weights(1234, "init")
+    pw = w["encoder.projection.weight"].copy()
+    pw[5, 17] = np.nan
+    w["encoder.projection.weight"] = pw
+    eng = pkg.Engine(img_hw=(384, 384), max_batch=2, precision="bf16x3", variant=variant, max_beam=max_beam)
+    eng.load_weights(w)
+    eng.encode(pkg.synth.make_images(2, 384, 384, seed0=1000))
+    assert np.isnan(eng.memory()[:, :, 5]).all()
+    with pytest.raises(pkg.MocrError, match="non-finite"):
+        eng.decode(max_steps=8, stop="none")
+    eng.close()

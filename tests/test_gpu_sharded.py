@@ -29,7 +29,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, stop="none"):
     try:
         sys.path.insert(0, REPO)
         os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -47,11 +47,16 @@ def _worker(rank, world, port, q):
         eng.load_weights(apply_eos_boost(pkg.synth.make_weights(m["seed"], m["variant"]), m["eos_boost"]))
         eng.encode(imgs)
         steps = g["ids"].shape[1] - 1
-        res = eng.decode(max_steps=steps, stop="none")
+        res = eng.decode(max_steps=steps if stop == "none" else m["steps"], stop=stop)
         eng.close()
-        gathered = pkg.parallel.gather_ids_host(torch.from_numpy(res.ids), world)
+        # a shard under the batch stop ends when its own rows have all finished (DESIGN.md
+        # §6): pad its ids to the fixture's width for the gather, and report its step count
+        ids = np.full((b - a, m["steps"] + 1), pkg.synth.PAD_ID, np.int32)
+        ids[:, :res.ids.shape[1]] = res.ids
+        gathered = pkg.parallel.gather_ids_host(torch.from_numpy(ids), world)
+        n_steps = pkg.parallel.gather_ids_host(torch.tensor([[res.n_steps]], dtype=torch.int32), world)
         if rank == 0:
-            q.put(("ok", gathered.numpy()))
+            q.put(("ok", (gathered.numpy(), n_steps.numpy().ravel())))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as ex:  # report instead of hanging the parent on the queue
@@ -59,12 +64,12 @@ def _worker(rank, world, port, q):
         raise
 
 
-def test_two_shards_on_one_gpu_match_fixture(golden):
+def _run_shards(stop):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, stop)) for r in range(2)]
     for p in procs:
         p.start()
     status, out = q.get(timeout=240)
@@ -72,6 +77,12 @@ def test_two_shards_on_one_gpu_match_fixture(golden):
         p.join(timeout=60)
     assert status == "ok", out
     assert all(p.exitcode == 0 for p in procs)
+    return out
+
+
+def test_two_shards_on_one_gpu_match_fixture(golden):
+    out, _ = _run_shards("none")
+    out = out[:, :golden("g96x320_b4_eos")["ids"].shape[1]]
     # rows are independent: the fixed-length decode of each shard equals the fixture's rows
     # (the fixture's batch-global stop only decides how many columns exist)
     g = golden("g96x320_b4_eos")
@@ -79,6 +90,28 @@ def test_two_shards_on_one_gpu_match_fixture(golden):
            if not np.array_equal(out[i], g["ids"][i])]
     # (row, first differing column, the fixture's top-2 logit margin at the step before it)
     assert not bad, [(i, c, float(g["margins"][i, c - 1])) for i, c in bad]
+
+
+def test_two_shards_batch_stop_each_shard_stops_on_its_own(pkg, golden):
+    """SURVEY §8(e) option 1: under the reference's batch-global stop
+    (src/inference.py:23-25) each shard stops once its own rows have all produced EOS, with
+    no collective; every row's tokens up to and including its EOS (its string) equal the
+    fixture's, whose stop was global over the 4 rows.  The shards' step counts may be
+    shorter than the fixture's, never longer."""
+    g = golden("g96x320_b4_eos")
+    out, n_steps = _run_shards("batch")
+    eos = pkg.synth.EOS_ID
+    n_fix = g["ids"].shape[1] - 1
+    assert (n_steps <= n_fix).all() and n_steps.max() == n_fix, (n_steps, n_fix)
+    for i in range(g["ids"].shape[0]):
+        ref = g["ids"][i]
+        hit = np.flatnonzero(ref[1:] == eos)
+        assert hit.size, f"fixture row {i} never reaches EOS"
+        end = int(hit[0]) + 2  # through the EOS column
+        np.testing.assert_array_equal(out[i, :end], ref[:end], err_msg=f"row {i}")
+    # the detokenised strings (cut at EOS) are the fixture's
+    vocab, idx2char = pkg.synth.synthetic_vocab()
+    assert [pkg.utils.detokenize(r.tolist(), idx2char) for r in out] == g["meta"]["strings"]
 
 
 def test_rccl_group_gather_one_rank(pkg):
