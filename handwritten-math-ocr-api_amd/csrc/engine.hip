@@ -283,6 +283,10 @@ struct mocr_engine {
   mocr_config cfg{};
   int device = 0;
   hipStream_t stream = nullptr;
+  // the engine stream's CU mask (mocr_set_cu_mask) and priority (mocr_set_stream_priority):
+  // HIP creates a stream with one or the other, so the two settings exclude each other
+  bool stream_cu_masked = false;
+  int stream_priority = 0;
   std::string err;
   std::unique_ptr<Layout> lay;
 
@@ -2031,6 +2035,9 @@ int mocr_debug_encode_until(mocr_engine* eng, int batch, int k, float* host_out,
 int mocr_set_cu_mask(mocr_engine* eng, const uint32_t* mask, int n_words) {
   MOCR_API_BODY(eng, {
     if (n_words < 0 || (n_words > 0 && !mask)) throw std::runtime_error("bad CU mask");
+    if (n_words && eng->stream_priority != 0)
+      throw std::runtime_error("mocr_set_cu_mask: the stream has a priority (mocr_set_stream_priority); HIP makes a "
+                               "stream with a CU mask or a priority, not both: set the priority to 0 first");
     MOCR_HIP_CHECK(hipSetDevice(eng->device));
     MOCR_HIP_CHECK(hipStreamSynchronize(eng->stream));
     hipStream_t s = nullptr;
@@ -2040,6 +2047,7 @@ int mocr_set_cu_mask(mocr_engine* eng, const uint32_t* mask, int n_words) {
       MOCR_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     MOCR_HIP_CHECK(hipStreamDestroy(eng->stream));
     eng->stream = s;
+    eng->stream_cu_masked = n_words != 0;
   })
 }
 
@@ -2051,11 +2059,16 @@ int mocr_set_stream_priority(mocr_engine* eng, int priority) {
     MOCR_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     // priority: 0 normal, > 0 higher (the device's greatest), < 0 lower (its least)
     const int prio = priority > 0 ? greatest : (priority < 0 ? least : 0);
+    if (priority != 0 && eng->stream_cu_masked)
+      throw std::runtime_error("mocr_set_stream_priority: the stream has a CU mask (mocr_set_cu_mask); HIP makes a "
+                               "stream with a CU mask or a priority, not both: clear the mask first");
     MOCR_HIP_CHECK(hipStreamSynchronize(eng->stream));
     hipStream_t s = nullptr;
     MOCR_HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio));
     MOCR_HIP_CHECK(hipStreamDestroy(eng->stream));
     eng->stream = s;
+    eng->stream_cu_masked = false;
+    eng->stream_priority = priority;
   })
 }
 

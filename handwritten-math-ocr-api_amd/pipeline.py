@@ -4,9 +4,8 @@ A greedy decode step is a chain of small, latency-bound kernels, while the encod
 throughput-bound stream of large GEMMs.  Calls are independent, so R engines on the same
 device, each driven by its own thread (ctypes releases the GIL; each engine has its own
 HIP stream), overlap one call's decode with another call's encoder.  The GPU time of the
-two halves still adds up: at 256 rows per call (4 batches of 64,
-384², bf16x3) and 2 replicas, encode-only 7551 img/s and decode-only 6988 img/s give
-3604 img/s together (tools/pipeline_probe.py, profiles/r03/pipeline_probe_rows256_r2.log).
+two halves still adds up rather than hiding one behind the other (DESIGN.md §5.5-5.6,
+tools/pipeline_probe.py measures encode-only, decode-only and both).
 
 ``imap`` preserves submission order, so callers can run an order-sensitive step
 (e.g. the RCCL gather of token streams in ``bench.py``) on the results, identically on

@@ -212,7 +212,9 @@ typedef struct mocr_kernel_stat {
 int mocr_set_timing(mocr_engine* eng, int enabled); /* also resets the counters */
 
 /* Restrict the engine's HIP stream to a set of CUs (hipExtStreamCreateWithCUMask: bit i
- * of mask[i / 32] enables CU i); n_words = 0 restores an unmasked stream. */
+ * of mask[i / 32] enables CU i); n_words = 0 restores an unmasked stream.  HIP makes a
+ * stream with a CU mask or a priority, not both: a mask on a stream with a non-zero
+ * priority (and a non-zero priority on a masked stream) fails. */
 int mocr_set_cu_mask(mocr_engine* eng, const uint32_t* mask, int n_words);
 
 /* Recreate the engine's stream at a HIP stream priority: > 0 the device's highest, < 0

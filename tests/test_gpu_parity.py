@@ -334,3 +334,27 @@ def test_predict_script_batch1(pkg, golden):
         expected = [idx2char[int(i)] for i in row[1:e]]
         assert pkg.predict.predict(imgs[r:r + 1], eng, vocab, idx2char) == expected
     eng.close()
+
+
+def test_cu_mask_and_priority_exclude_each_other(pkg):
+    """HIP makes an engine stream with a CU mask or a priority, not both: the
+    second setting fails instead of silently dropping the first; clearing one allows the
+    other, and the engine still decodes correctly on the rebuilt stream."""
+    g = pkg.synth
+    eng = pkg.Engine(img_hw=(96, 320), max_batch=1, precision="fp32")
+    eng.set_cu_mask(range(128))
+    with pytest.raises(pkg.MocrError, match="CU mask"):
+        eng.set_stream_priority(1)
+    eng.set_cu_mask(None)
+    eng.set_stream_priority(1)
+    with pytest.raises(pkg.MocrError, match="priority"):
+        eng.set_cu_mask(range(64))
+    eng.set_stream_priority(0)
+    eng.set_cu_mask(range(64))
+    eng.load_weights(g.make_weights(5, "perturbed"))
+    eng.encode(g.make_images(1, 96, 320, 1000, "ink"))
+    a = eng.decode(max_steps=4, stop="none").ids
+    eng.set_cu_mask(None)
+    b = eng.decode(max_steps=4, stop="none").ids
+    np.testing.assert_array_equal(a, b)
+    eng.close()

@@ -10,6 +10,12 @@ grep -E "PARITY_RECORD|passed|failed" $O/cond.log | tail -12
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread \
   > $O/tests.log 2>&1 || { echo "TESTS FAILED"; tail -40 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
+for L in production cn; do
+  A=""; [ $L = cn ] && A="--lib handwritten-math-ocr-api_amd/lib_var/cn/libmathocr.so"
+  timeout -k 10 240 python -u tools/decode_chain_probe.py --rows 256 --chains 1,2 --reps 2 $A > $O/chain_$L.log 2>&1 \
+    || { echo "CHAIN $L FAILED"; tail -20 $O/chain_$L.log; exit 1; }
+  echo "$L"; grep rows_per_s $O/chain_$L.log
+done
 timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > $O/bench_auto.json 2> $O/bench_auto.err \
   || { echo "BENCH FAILED"; tail -20 $O/bench_auto.err; exit 1; }
 cut -c1-300 $O/bench_auto.json
