@@ -10,9 +10,10 @@ then, with N > 1 ranks, an RCCL all-gather of the decoded token streams inside
 libmathocr.so (``mocr_group_gather_ids``; image-parallel shards, no other collective;
 torch.distributed over gloo carries only the group id, barriers and the timing max).
 
-Each engine call takes G = --chain-batches batches of 64 (default: 4, or 5 when that makes
-the timed batches a whole number of calls per replica, see ``auto_chain``): one encode of
-the G*64 images and ONE decode chain of G*64 rows.  A greedy step is a chain of 41 dependent
+Each engine call takes G = --chain-batches batches of 64 (default ``auto_chain``: the largest
+G <= 10 that makes the timed batches a whole number of calls per replica -- 8 at the default
+64 steps, 10 at the driver's 20): one encode of the G*64 images and ONE decode chain of
+G*64 rows.  A greedy step is a chain of 41 dependent
 kernels whose launch and memory latencies do not grow with the rows, so G batches in one
 chain amortise them G ways (profiles/r03/decode_chain_probe_*.log); rows are
 independent (stop="none" here; tests/test_gpu_parity.py::test_wide_chain_rows_bitwise
@@ -96,13 +97,16 @@ def parse():
     return a
 
 
-def auto_chain(steps, replicas):
-    """Batches per engine call: 4 (256-row decode chains), or 5 when 4 would leave the
-    timed calls uneven over the replicas and 5 does not.  An uneven count leaves the last
-    call's decode chain running alone at the end of the timed region (one 256-row chain
-    alone runs at ~60 % of two concurrent ones): --steps 20 is 5 calls of 4
-    (one replica runs 3) but 4 calls of 5 (2 each)."""
-    for g in (4, 5):
+def auto_chain(steps, replicas, g_max=10):
+    """Batches of 64 per engine call: the largest G <= g_max that splits the timed batches
+    into a whole number of calls per replica.  More images in flight raise throughput (a
+    decode step's 41 dependent launches cost little more at 512-640 rows than at 256, and
+    two concurrent chains overlap their latencies) at the cost of the call's latency: on one
+    box, 64 batches at 4 / 8 x 64 with 2 replicas gave 4410 / 4798-4889 img/s at p50 114 /
+    209-213 ms; 20 batches at 5 / 10 x 64 gave 4302 / 4807 img/s at p50 148 / 266 ms; four
+    replicas or 16 x 64 saturate near 4900 (profiles/r04/r04e-f).  Uneven calls per replica
+    leave the last call's decode chain alone at the end of the timed region."""
+    for g in range(g_max, 3, -1):
         if steps % g == 0 and (steps // g) % replicas == 0:
             return g
     return 4

@@ -80,7 +80,7 @@ def test_default_run_is_one_gpu_minutes_scale(bench, monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py"])
     a = bench.parse()
     assert a.gpus == 1 and a.steps == 64 and a.warmup == 4 and a.batch == 64 and a.tokens == 128
-    assert a.chain == 4 and a.replicas == 2 and a.precision == "bf16x3" and a.image == [384, 384]
+    assert a.chain == 8 and a.replicas == 2 and a.precision == "bf16x3" and a.image == [384, 384]
     assert a.cpu_sample == 64 and a.cpu_runs == 3  # B = 64, median of 3
     monkeypatch.setattr(sys, "argv", ["bench.py", "--arch", "res18trans"])
     a = bench.parse()
@@ -88,13 +88,13 @@ def test_default_run_is_one_gpu_minutes_scale(bench, monkeypatch):
 
 
 def test_auto_chain_keeps_timed_calls_even_over_replicas(bench, monkeypatch):
-    # the driver's --steps 20: 5 calls of 4 batches would leave one replica a third call
-    # whose decode chain runs alone; 4 calls of 5 give each replica 2
-    assert bench.auto_chain(20, 2) == 5 and bench.auto_chain(64, 2) == 4 and bench.auto_chain(8, 2) == 4
-    assert bench.auto_chain(7, 2) == 4
+    # the largest chain <= 10 batches that gives every replica the same number of calls:
+    # the driver's --steps 20 -> 2 calls of 10, the default 64 -> 8 calls of 8
+    assert bench.auto_chain(20, 2) == 10 and bench.auto_chain(64, 2) == 8 and bench.auto_chain(8, 2) == 4
+    assert bench.auto_chain(7, 2) == 4 and bench.auto_chain(40, 2) == 10 and bench.auto_chain(20, 4) == 5
     monkeypatch.setattr(sys, "argv", ["bench.py", "--steps", "20", "--warmup", "5"])
     a = bench.parse()
-    assert (a.chain, a.replicas) == (5, 2)
+    assert (a.chain, a.replicas) == (10, 2)
     monkeypatch.setattr(sys, "argv", ["bench.py", "--steps", "20", "--chain-batches", "4"])
     assert bench.parse().chain == 4
 
