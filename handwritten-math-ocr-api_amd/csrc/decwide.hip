@@ -145,7 +145,7 @@ struct TileLds {
 //    loaded before the first store: a load issued after a store waits for it (vmcnt).
 // MFMA operands: row / column = lane & 15, k = 8 g .. 8 g + 7 of the step (X3) or
 // 4 g .. 4 g + 3 (fp32), g = lane >> 4.
-template <int BM, int BN, bool YT, int K1, bool S1, bool S2, bool X3, bool LOGITS, int NW>
+template <int BM, int BN, bool YT, int K1, bool S1, bool S2, bool X3, bool LOGITS, int NW, int PD>
 __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c0, char* smem) {
   using L = TileLds<BM, BN, YT, K1, X3, NW>;
   constexpr int MF = BM / 16, NF = BN / 16;
@@ -191,10 +191,15 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
     if constexpr (S1) pa1[mf] = load_part4(p.a1_stats + (size_t)qrow[mf] * 2 * kSlices, c);
     if constexpr (S2 && !YT) pa2[mf] = load_part4(p.a2_stats + (size_t)qrow[mf] * 2 * kSlices, c);
   }
-  floatx4 ra[NKS][SPS][MF];
-  floatx4 rw[NKS][NF][X3 ? 2 : 1];
-#pragma unroll
-  for (int s = 0; s < NKS; ++s) {
+  // step s's A pieces and W fragments live in ring slot s % NR: the first NR steps are
+  // loaded up front, step s + NR's right after step s's MFMAs (PD < NKS trades that step's
+  // load latency for registers: the FFN kernel at 148 VGPRs holds one 8-wave workgroup per
+  // CU, at PD = 2 two, so a chain of more than 256 rows is still one round)
+  constexpr int NR = PD < NKS ? PD : NKS;
+  floatx4 ra[NR][SPS][MF];
+  floatx4 rw[NR][NF][X3 ? 2 : 1];
+  auto load_step = [&](int s) {
+    const int sl = s % NR;
 #pragma unroll
     for (int h = 0; h < SPS; ++h) {
       const int sg = s * SPS + h;
@@ -202,20 +207,22 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
       const bool in1 = kbeg + sg * 16 < K1;  // wave-uniform
 #pragma unroll
       for (int mf = 0; mf < MF; ++mf)
-        ra[s][h][mf] = *reinterpret_cast<const floatx4*>(in1 ? p.A1 + (size_t)qrow[mf] * K1 + k
-                                                             : p.A2 + (size_t)qrow[mf] * kD + (k - K1));
+        ra[sl][h][mf] = *reinterpret_cast<const floatx4*>(in1 ? p.A1 + (size_t)qrow[mf] * K1 + k
+                                                              : p.A2 + (size_t)qrow[mf] * kD + (k - K1));
     }
 #pragma unroll
     for (int nf = 0; nf < NF; ++nf) {
       const size_t fo = ((size_t)(wt0 + nf) * (ldw / KS) + kbeg / KS + s) * 64 + lane;
       if constexpr (X3) {
-        rw[s][nf][0] = reinterpret_cast<const floatx4*>(YT ? p.Fy_hi : p.Fz_hi)[fo];
-        rw[s][nf][1] = reinterpret_cast<const floatx4*>(YT ? p.Fy_lo : p.Fz_lo)[fo];
+        rw[sl][nf][0] = reinterpret_cast<const floatx4*>(YT ? p.Fy_hi : p.Fz_hi)[fo];
+        rw[sl][nf][1] = reinterpret_cast<const floatx4*>(YT ? p.Fy_lo : p.Fz_lo)[fo];
       } else {
-        rw[s][nf][0] = reinterpret_cast<const floatx4*>(YT ? p.Fy : p.Fz)[fo];
+        rw[sl][nf][0] = reinterpret_cast<const floatx4*>(YT ? p.Fy : p.Fz)[fo];
       }
     }
-  }
+  };
+#pragma unroll
+  for (int s = 0; s < NR; ++s) load_step(s);
   // epilogue operands (the first 256 threads: row = tid >> 4 of each 16-row block, column
   // = tid & 15 of each 16-column block)
   const int erow = (tid & 255) >> 4;
@@ -281,7 +288,7 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
       }
 #pragma unroll
       for (int mf = 0; mf < MF; ++mf) {
-        floatx4 x = ra[s][h][mf];
+        floatx4 x = ra[s % NR][h][mf];
 #ifdef MOCR_FOLD_NOXFORM  // timing probe: no LN / unfold transform, no split (wrong results)
         {
           const int lt = q + 16 * (h * 2 + (c >> 1));
@@ -332,9 +339,10 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
 #pragma unroll
           for (int nf = 0; nf < NF; ++nf) {
             const bf16x8 a = pass == 2 ? al[mf] : ah[mf];
-            const bf16x8 b = __builtin_bit_cast(bf16x8, rw[s][nf][pass == 1 ? 1 : 0]);
+            const bf16x8 b = __builtin_bit_cast(bf16x8, rw[s % NR][nf][pass == 1 ? 1 : 0]);
             acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[mf][nf], 0, 0, 0);
           }
+      if (s + NR < NKS) load_step(s + NR);
     } else {
       floatx4 a[MF];
 #pragma unroll
@@ -345,7 +353,8 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
         for (int mf = 0; mf < MF; ++mf)
 #pragma unroll
           for (int nf = 0; nf < NF; ++nf)
-            acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mf][e], rw[s][nf][0][e], acc[mf][nf], 0, 0, 0);
+            acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mf][e], rw[s % NR][nf][0][e], acc[mf][nf], 0, 0, 0);
+      if (s + NR < NKS) load_step(s + NR);
     }
   }
 
@@ -423,7 +432,7 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
   MOCR_TS(6, __builtin_amdgcn_s_memrealtime());
 }
 
-template <int BM, int BN, int K1, bool S1, bool S2, bool X3, bool LOGITS, int NW>
+template <int BM, int BN, int K1, bool S1, bool S2, bool X3, bool LOGITS, int NW, int PD>
 __global__ void __launch_bounds__(64 * NW) foldwide_kernel(FoldGemmParams p) {
   constexpr int BYTES = LOGITS ? TileLds<BM, BN, false, 0, X3, NW>::BYTES
                                : (TileLds<BM, BN, true, K1, X3, NW>::BYTES > TileLds<BM, BN, false, K1, X3, NW>::BYTES
@@ -435,12 +444,12 @@ __global__ void __launch_bounds__(64 * NW) foldwide_kernel(FoldGemmParams p) {
   const int c0 = (b % ncol) * BN;
   const int r0 = (b / ncol) * BM;
   if constexpr (LOGITS) {
-    wide_tile<BM, BN, false, 0, false, true, X3, true, NW>(p, r0, c0, smem);
+    wide_tile<BM, BN, false, 0, false, true, X3, true, NW, PD>(p, r0, c0, smem);
   } else {
     if (c0 < p.NY)
-      wide_tile<BM, BN, true, K1, S1, S2, X3, false, NW>(p, r0, c0, smem);
+      wide_tile<BM, BN, true, K1, S1, S2, X3, false, NW, PD>(p, r0, c0, smem);
     else
-      wide_tile<BM, BN, false, K1, S1, S2, X3, false, NW>(p, r0, c0, smem);
+      wide_tile<BM, BN, false, K1, S1, S2, X3, false, NW, PD>(p, r0, c0, smem);
   }
 }
 
@@ -470,24 +479,39 @@ __global__ void frag_pack_kernel(const float* __restrict__ W, int N, int K, uint
   }
 }
 
-template <int BM, int BN, bool X3, bool LOGITS, int NW>
-void launch_fw_nw(const FoldGemmParams& p, hipStream_t s) {
+template <int BM, int BN, bool X3, bool LOGITS, int NW, int PD>
+void launch_fw_pd(const FoldGemmParams& p, hipStream_t s) {
   const int ncol = (p.NY + p.NZ) / BN;
   const dim3 grid(ncol * ((p.B + BM - 1) / BM));
   if constexpr (LOGITS) {
-    foldwide_kernel<BM, BN, 0, false, true, X3, true, NW><<<grid, 64 * NW, 0, s>>>(p);
+    foldwide_kernel<BM, BN, 0, false, true, X3, true, NW, PD><<<grid, 64 * NW, 0, s>>>(p);
   } else {
     const bool s1 = p.a1_stats != nullptr, s2 = p.a2_stats != nullptr;
     if (p.K1 == 256 && !s1 && !s2) {
-      foldwide_kernel<BM, BN, 256, false, false, X3, false, NW><<<grid, 64 * NW, 0, s>>>(p);
+      foldwide_kernel<BM, BN, 256, false, false, X3, false, NW, PD><<<grid, 64 * NW, 0, s>>>(p);
     } else if (p.K1 == 256 && !s1 && s2) {
-      foldwide_kernel<BM, BN, 256, false, true, X3, false, NW><<<grid, 64 * NW, 0, s>>>(p);
+      foldwide_kernel<BM, BN, 256, false, true, X3, false, NW, PD><<<grid, 64 * NW, 0, s>>>(p);
     } else if (p.K1 == 512 && s1 && s2) {
-      foldwide_kernel<BM, BN, 512, true, true, X3, false, NW><<<grid, 64 * NW, 0, s>>>(p);
+      foldwide_kernel<BM, BN, 512, true, true, X3, false, NW, PD><<<grid, 64 * NW, 0, s>>>(p);
     } else {
       throw std::runtime_error("foldwide: built for (K1 256, A2 plain or LayerNorm), (K1 512, both), logits");
     }
   }
+}
+
+// the FFN kernel (K1 = 512, 32 x 32 tiles, 8 waves) with every k step's loads in flight
+// holds one workgroup per CU; above 256 workgroups (chains of more than 256 rows) it keeps
+// two k steps in flight instead, which fits two (profiles/r04/r04h)
+template <int BM, int BN, bool X3, bool LOGITS, int NW>
+void launch_fw_nw(const FoldGemmParams& p, hipStream_t s) {
+  if constexpr (!LOGITS && NW == 8 && BM == 32 && BN == 32) {
+    const int nblk = (p.NY + p.NZ) / BN * ((p.B + BM - 1) / BM);
+    if (p.K1 == 512 && nblk > 256 && !p.no_prefetch_ring) {
+      launch_fw_pd<BM, BN, X3, LOGITS, NW, 2>(p, s);
+      return;
+    }
+  }
+  launch_fw_pd<BM, BN, X3, LOGITS, NW, 8>(p, s);
 }
 
 // NW waves split K (p.waves: 4 or 8; 0 = kWideWaves).  The same NW at every row count, so

@@ -251,6 +251,7 @@ struct FoldGemmParams {
   const float *Fy, *Fz;
   int waves;      // launch_foldwide: waves splitting K (0: the default; tools/wide_bench A/B 4 vs 8)
   int tile_cols;  // launch_foldwide logits: columns per tile, 32 / 64 / 128 (0: the default; A/B)
+  int no_prefetch_ring;  // launch_foldwide: every k step's loads up front at any grid (A/B)
   // bf16x3 (optional): bf16 hi / lo planes of Wy and Wz; A is split on load and each
   // product is hi·hi + hi·lo + lo·hi on v_mfma_f32_16x16x32_bf16 (fp32 MFMA otherwise)
   const uint16_t *Wy_hi, *Wy_lo, *Wz_hi, *Wz_lo;
