@@ -456,8 +456,11 @@ struct mocr_engine {
       RTl = dalloc<uint16_t>(szmap);
     }
     rzero = dalloc<char>(256);
-    MOCR_HIP_CHECK(hipMemset(rzero, 0, 256));
-    MOCR_HIP_CHECK(hipDeviceSynchronize());  // null-stream memset vs the engine's non-blocking stream
+    // on the engine's stream: a kernel on the null stream claims one of the process's
+    // hardware queues (GPU_MAX_HW_QUEUES, 4), and engines created after it then share
+    // queues (profiles/r04/r04i: config 4's four replicas on three queues)
+    MOCR_HIP_CHECK(hipMemsetAsync(rzero, 0, 256, stream));
+    MOCR_HIP_CHECK(hipStreamSynchronize(stream));
     RP = dalloc<float>(rows * 512);
     RPOS = dalloc<float>((size_t)M * d);
     RPOSB = dalloc<float>(rows * d);
@@ -787,8 +790,9 @@ struct mocr_engine {
       for (int i = 0; i < 2; ++i) {
         bseq[i] = dalloc<int32_t>(R * ld_ids);
         bslot[i] = dalloc<int32_t>(R * ld_ids);
-        MOCR_HIP_CHECK(hipMemset(bseq[i], 0, R * ld_ids * sizeof(int32_t)));
-        MOCR_HIP_CHECK(hipMemset(bslot[i], 0, R * ld_ids * sizeof(int32_t)));
+        // engine stream, not the null stream (see init_res18's rzero)
+        MOCR_HIP_CHECK(hipMemsetAsync(bseq[i], 0, R * ld_ids * sizeof(int32_t), stream));
+        MOCR_HIP_CHECK(hipMemsetAsync(bslot[i], 0, R * ld_ids * sizeof(int32_t), stream));
       }
     }
     if (fold_greedy()) {
@@ -834,7 +838,7 @@ struct mocr_engine {
     st = dalloc<DecodeState>(1);
     MOCR_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&st_host), 2 * sizeof(DecodeState), hipHostMallocDefault));
     for (auto& e : chunk_ev) MOCR_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    MOCR_HIP_CHECK(hipDeviceSynchronize());  // null-stream memsets above vs the non-blocking stream
+    MOCR_HIP_CHECK(hipStreamSynchronize(stream));  // the setup memsets above
   }
 
   // [type][h][64 q][64 key] table of the bf16 attention kernel: bias[h][q][key] plus the
