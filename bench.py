@@ -186,11 +186,13 @@ def cpu_baseline(args, pkg):
                       f"fp32 torch CPU, {threads} threads; {n}-image run {thr:.1f} s"}
 
 
-def pmc_traffic(precision, cls):
-    """HBM bytes per launch of a kernel class from the committed rocprofv3 PMC passes
-    (profiles/pmc_traffic_<precision>.json, written by tools/pmc_traffic.py: FETCH_SIZE x2
-    + WRITE_SIZE), or None when no such profile exists."""
-    path = os.path.join(REPO, "profiles", f"pmc_traffic_{precision}.json")
+def pmc_traffic(precision, cls, batch):
+    """HBM bytes per launch of a kernel class from the committed rocprofv3 PMC passes of
+    an encode of `batch` images and 8 greedy steps over them
+    (profiles/pmc_traffic_<precision>_b<batch>.json, written by tools/pmc_traffic.py:
+    FETCH_SIZE x2 + WRITE_SIZE), or None when no profile of that batch exists (bytes per
+    launch depend on the batch)."""
+    path = os.path.join(REPO, "profiles", f"pmc_traffic_{precision}_b{batch}.json")
     try:
         return json.load(open(path))["classes"][cls]["hbm_bytes_per_launch"]
     except (OSError, KeyError, ValueError):
@@ -202,7 +204,7 @@ def pmc_traffic(precision, cls):
 E2E_ROOFLINE_IMG_S = 1.0 / (26.39e9 / 2.5e15 + 245e6 / 8e12)
 
 
-def roofline(stats, dtype, precision, attention=False):
+def roofline(stats, dtype, precision, batch, attention=False):
     """Dominant encoder GEMM class (attention=False) or window-attention class
     (attention=True: the fused norm1 + qkv + W-MSA kernels, s3.attn at 384²) by
     event-timed GPU time: algorithmic FLOP per launch / average launch duration, against
@@ -224,7 +226,7 @@ def roofline(stats, dtype, precision, attention=False):
     out = {"kernel": f"{kind}[{dtype}] {name}", "bound": "mfma",
            "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
            "peak_basis": "dense fp32 MFMA" if dtype == "f32" else "dense bf16 MFMA (2.5 PF)",
-           "traffic": pmc_traffic(precision, name),
+           "traffic": pmc_traffic(precision, name, batch),
            "avg_launch_ms": avg_ms, "flops_per_launch": flops,
            "algorithmic_bytes_per_launch": d["bytes"] / d["launches"]}
     if dtype == "bf16x3":
@@ -255,7 +257,7 @@ def roofline_decode(stats, precision, rows, steps):
     return {"kernel": f"greedy decode step over {rows} rows (8 layers x 5 folded kernels + logits; the selection "
                       f"runs in the next step's first kernel)", "bound": "hbm",
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "traffic": pmc_traffic(precision, "decode.step"), "avg_step_ms": step_ms, "rows": rows,
+            "traffic": pmc_traffic(precision, "decode.step", rows), "avg_step_ms": step_ms, "rows": rows,
             "algorithmic_bytes_per_step": survey, "bytes_basis": "SURVEY.md §8(d): bf16 weights and K/V",
             "as_built_bytes_per_step": built, "as_built_achieved": built / (step_ms * 1e-3) / 1e9,
             "as_built_frac": built / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -473,8 +475,8 @@ def main():
                            f"outside the timed region; serialised with the calls it would give "
                            f"{BG * calls / (elapsed + calls * h2d * 1e-3) * world:.0f} img/s (pageable source)")
         rd = roofline_decode(iso["stats"], args.precision, BG, S)
-        rg = roofline(iso["stats"], dtype, args.precision)
-        ra = roofline(iso["stats"], dtype, args.precision, attention=True)
+        rg = roofline(iso["stats"], dtype, args.precision, BG)
+        ra = roofline(iso["stats"], dtype, args.precision, BG, attention=True)
         # `roofline` is the dominant kernel class by GPU time (HIP events, one call alone):
         # the decode step when its share is the largest, else the dominant encoder GEMM
         dec_ms = iso["stats"].get("decode.greedy", {}).get("total_ms", 0.0)

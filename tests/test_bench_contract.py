@@ -36,7 +36,7 @@ def stats():
 
 
 def test_gemm_roofline_is_the_dominant_gemm_class(bench):
-    r = bench.roofline(stats(), "bf16x3", "bf16x3")
+    r = bench.roofline(stats(), "bf16x3", "bf16x3", 64)
     assert r["kernel"] == "gemm_bf16[bf16x3] s3.fc1" and r["bound"] == "mfma" and r["unit"] == "TFLOP/s"
     assert r["achieved"] == pytest.approx(43.486543872e9 / 162e-6 / 1e12)
     assert r["peak"] == 2500.0 and r["frac"] == pytest.approx(r["achieved"] / 2500.0)
@@ -45,10 +45,10 @@ def test_gemm_roofline_is_the_dominant_gemm_class(bench):
 
 
 def test_attention_roofline_is_the_dominant_attention_class(bench):
-    r = bench.roofline(stats(), "bf16x3", "bf16x3", attention=True)
+    r = bench.roofline(stats(), "bf16x3", "bf16x3", 64, attention=True)
     assert r["kernel"] == "attention[bf16x3] s3.attn"
     assert r["achieved"] == pytest.approx(35.38944e9 / 286e-6 / 1e12)
-    assert bench.roofline({"s3.fc1": rec(1, 0.1, 1e9)}, "bf16x3", "bf16x3", attention=True) is None
+    assert bench.roofline({"s3.fc1": rec(1, 0.1, 1e9)}, "bf16x3", "bf16x3", 64, attention=True) is None
 
 
 def test_decode_roofline_against_hbm(bench):
@@ -70,10 +70,14 @@ def test_e2e_roofline_is_baseline_md_section4(bench):
 
 
 def test_committed_pmc_traffic_covers_the_roofline_classes(bench):
-    for cls in ("s3.mlp", "s1.attn", "s3.lnqkv", "decode.step"):  # the bench's roofline classes at B = 256
-        t = bench.pmc_traffic("bf16x3", cls)
-        assert t is not None and t > 0, cls
-    assert bench.pmc_traffic("bf16x3", "no.such.class") is None
+    # the bench's roofline classes at its default 8 x 64 and the driver's 10 x 64 images per
+    # call (round 3's 4 x 64 profile kept)
+    for batch in (256, 512, 640):
+        for cls in ("s3.mlp", "s1.attn", "s3.lnqkv", "decode.step"):
+            t = bench.pmc_traffic("bf16x3", cls, batch)
+            assert t is not None and t > 0, (batch, cls)
+    assert bench.pmc_traffic("bf16x3", "no.such.class", 512) is None
+    assert bench.pmc_traffic("bf16x3", "s3.mlp", 333) is None
 
 
 def test_default_run_is_one_gpu_minutes_scale(bench, monkeypatch):

@@ -2,7 +2,7 @@
 
     rocprofv3 --pmc FETCH_SIZE --output-format csv -d F -o run -- python tools/profile_encoder.py
     rocprofv3 --pmc WRITE_SIZE --output-format csv -d W -o run -- python tools/profile_encoder.py
-    python tools/pmc_traffic.py F/run_counter_collection.csv W/run_counter_collection.csv OUT.json
+    python tools/pmc_traffic.py F/run_counter_collection.csv W/run_counter_collection.csv OUT.json [STEPS [BATCH]]
 
 Corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts 64 B per 128-B request for
 wide (16 B/lane) streaming reads on gfx950, so it is doubled; WRITE_SIZE is taken as is
@@ -51,7 +51,7 @@ def with_memkv24(names, kn):
     return names + ["memkv(fp24)"] * n + ["memkv(i16)"] * q
 
 
-def main(fetch_csv, write_csv, out, decode_steps=0):
+def main(fetch_csv, write_csv, out, decode_steps=0, batch=0):
     decode_steps = int(decode_steps)
     # engine dispatches only (the load-time decoder weight folding is not an encoder kernel)
     keep = lambda r: "mocr" in r["Kernel_Name"] and "fold_mm" not in r["Kernel_Name"] and "frag_pack" not in r["Kernel_Name"]
@@ -108,10 +108,10 @@ def main(fetch_csv, write_csv, out, decode_steps=0):
         d["hbm_bytes_per_launch"] = (d["fetch_bytes"] + d["write_bytes"]) / decode_steps
         for dk in dec_kernels.values():
             dk["hbm_bytes_per_launch"] = (dk["fetch_bytes"] + dk["write_bytes"]) / dk["launches"]
-    json.dump({"source": [os.path.relpath(p, os.path.dirname(os.path.abspath(out))) for p in (fetch_csv, write_csv)],
+    json.dump({"batch": int(batch), "source": [os.path.relpath(p, os.path.dirname(os.path.abspath(out))) for p in (fetch_csv, write_csv)],
                "fetch_correction": 2.0, "decode_steps": decode_steps, "classes": agg, "decode_kernels": dec_kernels},
               open(out, "w"), indent=1)
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    main(*sys.argv[1:6])
