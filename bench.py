@@ -288,11 +288,7 @@ def main():
             # group instead (only on a box with fewer GPUs than ranks; tests/test_gpu_sharded.py)
             gather = "gloo host (ranks share a device)"
         else:
-            grp = pkg.parallel.RcclGroup(world, rank, local)  # RCCL inside libmathocr.so
             gather = "rccl (mocr_group_gather_ids)"
-            rccl_ranks = grp.size()  # ncclCommCount
-            if rccl_ranks != world:
-                raise SystemExit(f"RCCL communicator counts {rccl_ranks} ranks, WORLD_SIZE is {world}")
     H, W = args.image
     B, S, R, G = args.batch, args.tokens, args.replicas, args.chain
     BG = B * G  # images per engine call (one encode, one decode chain of BG rows)
@@ -306,6 +302,13 @@ def main():
     ekw = dict(img_hw=(H, W), max_batch=BG, precision=args.precision, device=local, arch=args.arch,
                max_beam=args.beam, max_pos=max_pos)
     pool = pkg.pipeline.ReplicaPool(R, **ekw)
+    if gather.startswith("rccl"):
+        # after the engines: their HIP streams take the process's first hardware queues
+        # (GPU_MAX_HW_QUEUES = 4), the group's stream and RCCL's own come after them
+        grp = pkg.parallel.RcclGroup(world, rank, local)  # RCCL inside libmathocr.so
+        rccl_ranks = grp.size()  # ncclCommCount
+        if rccl_ranks != world:
+            raise SystemExit(f"RCCL communicator counts {rccl_ranks} ranks, WORLD_SIZE is {world}")
     weights = pkg.synth.make_weights(1234, "init", arch=args.arch, max_pos=max_pos)
     pool.load_weights(weights)
     # each replica holds its own G batches of this rank's shard, resident in HBM

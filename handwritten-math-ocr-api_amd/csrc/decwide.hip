@@ -520,7 +520,13 @@ void launch_fw_nw(const FoldGemmParams& p, hipStream_t s) {
 // (FFN at 256 rows 9.1 -> 7.5 us), 4 for the logits (10.8 vs 11.8 us)
 template <int BM, int BN, bool X3, bool LOGITS>
 void launch_fw(const FoldGemmParams& p, hipStream_t s) {
-  if ((p.waves ? p.waves : (LOGITS ? 4 : 8)) == 8)
+#ifndef MOCR_FOLD_WAVES  // A/B builds (tools/build_variant.sh DIR -DMOCR_FOLD_WAVES=4)
+#define MOCR_FOLD_WAVES 8
+#endif
+#ifndef MOCR_LOGITS_WAVES
+#define MOCR_LOGITS_WAVES 4
+#endif
+  if ((p.waves ? p.waves : (LOGITS ? MOCR_LOGITS_WAVES : MOCR_FOLD_WAVES)) == 8)
     launch_fw_nw<BM, BN, X3, LOGITS, 8>(p, s);
   else
     launch_fw_nw<BM, BN, X3, LOGITS, 4>(p, s);
