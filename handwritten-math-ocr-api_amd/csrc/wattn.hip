@@ -81,6 +81,12 @@ __device__ __forceinline__ void wfrag_perm(const uint16_t* hi, const uint16_t* l
   }
 }
 
+// timing probes of swin_attn_kernel (tools/build_variant.sh DIR -DMOCR_WATTN_PROBE=N; wrong
+// results): 1 no X loads (LN of zeros), 2 no qkv MFMAs, 3 no attention (S, softmax, PV),
+// 4 no proj MFMAs, 5 no weight loads (qkv and proj fragments from registers)
+#ifndef MOCR_WATTN_PROBE
+#define MOCR_WATTN_PROBE 0
+#endif
 template <int C, int PASSES, int OCC>
 __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC))) swin_attn_kernel(SwinAttnParams p) {
   constexpr bool X3 = PASSES == 3;
@@ -131,7 +137,7 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
       const float* src = p.X + (size_t)(px[ps] < 0 ? 0 : px[ps]) * C + c0;  // clamped, masked below
 #pragma unroll
       for (int e = 0; e < 3; ++e) {
-        const floatx4 t = *reinterpret_cast<const floatx4*>(src + 4 * e);
+        const floatx4 t = MOCR_WATTN_PROBE == 1 ? floatx4{1.f, 2.f, 3.f, 4.f} : *reinterpret_cast<const floatx4*>(src + 4 * e);
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[ps][4 * e + k] = t[k];
       }
@@ -200,13 +206,16 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
     for (int ks = 0; ks < HEADS; ++ks) {
       bf16x8 w[2][2];
 #pragma unroll
-      for (int f = 0; f < 2; ++f) wfrag<X3>(wqh, wql, C, row0 + 16 * f + j16, 32 * ks + 8 * g, w[f]);
+      for (int f = 0; f < 2; ++f) {
+        if constexpr (MOCR_WATTN_PROBE == 5) w[f][0] = w[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)ks, 1u, 2u, 3u});
+        else wfrag<X3>(wqh, wql, C, row0 + 16 * f + j16, 32 * ks + 8 * g, w[f]);
+      }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         bf16x8 xf[2];
         xfrag(ks, t, xf);
 #pragma unroll
-        for (int f = 0; f < 2; ++f) acc[f][t] = mma<X3>(w[f], xf, acc[f][t]);
+        for (int f = 0; f < 2; ++f) acc[f][t] = MOCR_WATTN_PROBE == 2 ? acc[f][t] + xf[0][0] : mma<X3>(w[f], xf, acc[f][t]);
       }
     }
   };
@@ -238,13 +247,16 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
     for (int ks = 0; ks < HEADS; ++ks) {
       bf16x8 w[2][2];
 #pragma unroll
-      for (int f = 0; f < 2; ++f) wfrag<X3>(wqh, wql, C, 2 * C + 32 * h + 16 * f + j16, 32 * ks + 8 * g, w[f]);
+      for (int f = 0; f < 2; ++f) {
+        if constexpr (MOCR_WATTN_PROBE == 5) w[f][0] = w[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)ks, 1u, 2u, 3u});
+        else wfrag<X3>(wqh, wql, C, 2 * C + 32 * h + 16 * f + j16, 32 * ks + 8 * g, w[f]);
+      }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         bf16x8 xf[2];
         xfrag(ks, t, xf);
 #pragma unroll
-        for (int f = 0; f < 2; ++f) acc[t][f] = mma<X3>(xf, w[f], acc[t][f]);
+        for (int f = 0; f < 2; ++f) acc[t][f] = MOCR_WATTN_PROBE == 2 ? acc[t][f] + xf[0][0] : mma<X3>(xf, w[f], acc[t][f]);
       }
     }
 #pragma unroll
@@ -294,6 +306,12 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
         bm[kt] = *reinterpret_cast<const floatx4*>(tb + (16 * qt + j16) * 64 + 16 * kt + 4 * g);
+    }
+    if constexpr (MOCR_WATTN_PROBE == 3) {
+      const int off = ((qt * HEADS + h) * 64 + lane) * 16;
+      *reinterpret_cast<bf16x8*>(lds + off) = kf[qt][0];
+      if constexpr (X3) *reinterpret_cast<bf16x8*>(lds + XB + off) = qf4[qt][1];
+      continue;
     }
     floatx4 st[4];
 #pragma unroll
@@ -370,7 +388,10 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
   for (int hh = 0; hh < HEADS; ++hh) {
     bf16x8 wa[2][2];
 #pragma unroll
-    for (int f = 0; f < 2; ++f) wfrag_perm<X3>(wph, wpl, C, 32 * h + 16 * f + j16, 32 * hh + 4 * g, wa[f]);
+    for (int f = 0; f < 2; ++f) {
+      if constexpr (MOCR_WATTN_PROBE == 5) wa[f][0] = wa[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)hh, 1u, 2u, 3u});
+      else wfrag_perm<X3>(wph, wpl, C, 32 * h + 16 * f + j16, 32 * hh + 4 * g, wa[f]);
+    }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       bf16x8 of[2];
@@ -378,7 +399,7 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
       of[0] = *reinterpret_cast<const bf16x8*>(lds + off);
       if constexpr (X3) of[1] = *reinterpret_cast<const bf16x8*>(lds + XB + off);
 #pragma unroll
-      for (int f = 0; f < 2; ++f) ap[f][t] = mma<X3>(wa[f], of, ap[f][t]);
+      for (int f = 0; f < 2; ++f) ap[f][t] = MOCR_WATTN_PROBE == 4 ? ap[f][t] + of[0][0] : mma<X3>(wa[f], of, ap[f][t]);
     }
   }
   __builtin_amdgcn_s_setprio(0);
@@ -529,7 +550,7 @@ swin_attn_noproj_kernel(SwinAttnParams p) {
       const float* src = p.X + (size_t)(px[ps] < 0 ? 0 : px[ps]) * C + c0;  // clamped, masked below
 #pragma unroll
       for (int e = 0; e < 3; ++e) {
-        const floatx4 t = *reinterpret_cast<const floatx4*>(src + 4 * e);
+        const floatx4 t = MOCR_WATTN_PROBE == 1 ? floatx4{1.f, 2.f, 3.f, 4.f} : *reinterpret_cast<const floatx4*>(src + 4 * e);
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[ps][4 * e + k] = t[k];
       }
@@ -599,13 +620,16 @@ swin_attn_noproj_kernel(SwinAttnParams p) {
     for (int ks = 0; ks < HEADS; ++ks) {
       bf16x8 w[2][2];
 #pragma unroll
-      for (int f = 0; f < 2; ++f) wfrag<X3>(wqh, wql, C, row0 + 16 * f + j16, 32 * ks + 8 * g, w[f]);
+      for (int f = 0; f < 2; ++f) {
+        if constexpr (MOCR_WATTN_PROBE == 5) w[f][0] = w[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)ks, 1u, 2u, 3u});
+        else wfrag<X3>(wqh, wql, C, row0 + 16 * f + j16, 32 * ks + 8 * g, w[f]);
+      }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         bf16x8 xf[2];
         xfrag(ks, t, xf);
 #pragma unroll
-        for (int f = 0; f < 2; ++f) acc[f][t] = mma<X3>(w[f], xf, acc[f][t]);
+        for (int f = 0; f < 2; ++f) acc[f][t] = MOCR_WATTN_PROBE == 2 ? acc[f][t] + xf[0][0] : mma<X3>(w[f], xf, acc[f][t]);
       }
     }
   };
