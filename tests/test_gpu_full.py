@@ -123,6 +123,33 @@ def test_config2_as_benched_b256_chain(pkg, golden):
     eng.close()
 
 
+def test_config2_as_benched_640_chain(pkg, golden):
+    """Config 2 the way the driver's `bench.py --steps 20` runs it: ten 64-image batches
+    encoded as one 640-image batch and decoded as one 640-row chain (above 256 rows the
+    FFN fold GEMM keeps two k steps in flight, decwide.hip launch_fw_nw; the MFMA sequence
+    per output is the same).  Rows 0-63 are the fixture's images."""
+    g = golden("g384_b64_bench")
+    imgs = pkg.synth.make_images(640, 384, 384, seed0=1000)
+    eng = pkg.Engine(img_hw=(384, 384), max_batch=640, precision="bf16x3")
+    eng.load_weights(pkg.synth.make_weights(1234, "init"))
+    eng.encode(imgs)
+    assert rel_err(eng.memory()[:2], g["memory"]) < 1e-4
+    res = eng.decode(max_steps=128, stop="none")
+    rec = {"config": "C2 as benched by the driver (B=640 encode, 640-row chain)", "precision": "bf16x3"}
+    n_full = check_ids(res.ids[:64], g["ids"], g["margins"], tie=1e-4, record=rec)
+    assert n_full >= 60, n_full
+    assert rec["rows_equal_all_columns"] >= C2_ROWS_EQUAL_FLOOR["bf16x3"], rec
+    # the last 64 rows decode as they do in a 64-row chain of their own (rows are
+    # independent: same memory bits, same per-row k order at any chain length)
+    e64 = pkg.Engine(img_hw=(384, 384), max_batch=64, precision="bf16x3", variant=("s3_large_batch",))
+    e64.load_weights(pkg.synth.make_weights(1234, "init"))
+    e64.encode(imgs[576:])
+    r64 = e64.decode(max_steps=128, stop="none")
+    e64.close()
+    eng.close()
+    np.testing.assert_array_equal(res.ids[576:], r64.ids)
+
+
 def test_config5_res18trans_b64_greedy128(pkg, golden):
     g = golden("r384_b64_bench")
     m = g["meta"]

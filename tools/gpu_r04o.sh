@@ -10,4 +10,8 @@ for L in production wp1 wp2 wp3 wp4 wp5; do
     || { echo "OPS $L FAILED"; tail $O/ops_$L.log; exit 1; }
   echo "== $L"; grep -E "attn" $O/ops_$L.log
 done
+
+timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_full.py -k "640_chain" > $O/test640.log 2>&1 \
+  || { echo "TEST640 FAILED"; tail -30 $O/test640.log; exit 1; }
+tail -3 $O/test640.log
 echo done
