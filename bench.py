@@ -83,6 +83,8 @@ def parse():
                     help="res18trans: BASELINE config 5 (src/model_res18trans.py)")
     ap.add_argument("--beam", type=int, default=0,
                     help="K > 0: beam search (BASELINE config 4: --beam 4 --batch 32 --tokens 256)")
+    ap.add_argument("--lib", default=None,
+                    help="an in-tree A/B build of libmathocr.so (tools/build_variant.sh) instead of lib/")
     a = ap.parse_args()
     if a.beam and a.arch != "swin":
         ap.error("--beam is measured on the Swin path")
@@ -277,6 +279,8 @@ def main():
     local = local % ndev
     dev = f"cuda:{local}"
     pkg = importlib.import_module("handwritten-math-ocr-api_amd")
+    if args.lib:
+        pkg.engine.load_library(args.lib)
     grp = None
     gather = "none"
     rccl_ranks = None

@@ -401,7 +401,9 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
         const int zc = ocol - p.NY;
         const float v = val + ebias[nf];
         const bool cv = zc < p.n_valid;
-        if (orow < B && cv) p.z[(p.hist_stride ? (size_t)p.t * p.hist_stride : 0) + (size_t)orow * p.NZ + zc] = v;
+        // z null: the greedy step without a logits history, whose selection reads only
+        // the tile partials (select.h), stores no logits row
+        if (p.z && orow < B && cv) p.z[(p.hist_stride ? (size_t)p.t * p.hist_stride : 0) + (size_t)orow * p.NZ + zc] = v;
         if (p.part) {
           // the 16-column tile's (max, first argmax, sum exp(l - max)) over the row's 16
           // lanes (DPP quad_perm xor 1, xor 2, row_half_mirror, row_mirror)
@@ -539,8 +541,8 @@ void launch_foldwide(const FoldGemmParams& p, hipStream_t s) {
   const bool logits = p.K1 == 0;
   const bool x3 = logits ? p.Fz_hi != nullptr : p.Fy_hi != nullptr;
   if (logits) {
-    if (p.NY != 0 || !p.a2_stats || !p.a2_g || !p.a2_b || !p.A2 || !p.bz || !p.z || p.NZ % 32 != 0)
-      throw std::runtime_error("foldwide logits: A2 with LayerNorm, no y, NZ % 32 == 0");
+    if (p.NY != 0 || !p.a2_stats || !p.a2_g || !p.a2_b || !p.A2 || !p.bz || !(p.z || p.part) || p.NZ % 32 != 0)
+      throw std::runtime_error("foldwide logits: A2 with LayerNorm, no y, z or partials, NZ % 32 == 0");
   } else {
     if (p.NY != kD || p.NZ % 32 != 0 || (p.NZ && (!p.bz || !p.z)))
       throw std::runtime_error("foldwide: NY == d and NZ a multiple of 32 with bz, z");
@@ -578,7 +580,15 @@ void launch_foldwide(const FoldGemmParams& p, hipStream_t s) {
         if (x3) launch_fw<16, 32, true, false>(p, s); else launch_fw<16, 32, false, false>(p, s);
       }
     } else {
-      if (narrow_n) {
+#ifndef MOCR_FFN_BN64  // A/B builds: the FFN fold GEMM on 32 x 64 tiles above 256 rows
+#define MOCR_FFN_BN64 0
+#endif
+      // 32 x 64 tiles: half the workgroups (one per CU at 512 rows) and half the A
+      // transform (the unfold runs once per row and column tile), the same k order per
+      // output element (the NW-wave K split does not depend on the tile width)
+      if (MOCR_FFN_BN64 && p.K1 == 512 && p.B > 256 && (p.NY + p.NZ) % 512 == 0) {
+        if (x3) launch_fw<32, 64, true, false>(p, s); else launch_fw<32, 64, false, false>(p, s);
+      } else if (narrow_n) {
         if (x3) launch_fw<32, 16, true, false>(p, s); else launch_fw<32, 16, false, false>(p, s);
       } else {
         if (x3) launch_fw<32, 32, true, false>(p, s); else launch_fw<32, 32, false, false>(p, s);

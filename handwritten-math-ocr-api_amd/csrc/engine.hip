@@ -1121,9 +1121,13 @@ struct mocr_engine {
   // at B = 256 1054 vs 903 us (ln1 + qkv GEMM + window attention over the image tokens,
   // tools/op_times.py --batch 256, profiles/r03/op_times_b256.log): the fused kernel
   // re-streams W_qkv per window, the GEMM's efficiency grows with M
+#ifndef MOCR_S3_FUSED_ATTN_LARGE  // A/B builds: the fused stage-3 attention at every batch
+#define MOCR_S3_FUSED_ATTN_LARGE 0
+#endif
   bool noproj_fused(int C, int B) const {
     return attn_fused() && swin_attn_noproj_supported(C) &&
-           (C != 768 || (cfg.variant & MOCR_VARIANT_S4_FUSED_ATTN)) && (C != 384 || !s3_large(B));
+           (C != 768 || (cfg.variant & MOCR_VARIANT_S4_FUSED_ATTN)) &&
+           (C != 384 || !s3_large(B) || MOCR_S3_FUSED_ATTN_LARGE);
   }
   // stage 3's kernels for >= 128 images: the unfused attention (above) and mlp.hip's fused
   // C = 384 MLP, which runs 128 rows per workgroup on all 256 CUs (1152 workgroups at
@@ -1584,7 +1588,10 @@ struct mocr_engine {
       FoldGemmParams g{};
       g.B = B; g.t = t; g.st = stp; g.K1 = 0; g.NY = 0;
       g.A2 = dy_ff; g.a2_stats = ds_ff; g.a2_g = W(last.n3w); g.a2_b = W(last.n3b);
-      g.Wz = fcw_pad; g.bz = fcb_pad; g.z = out; g.NZ = Vpad; g.n_valid = cfg.vocab; g.hist_stride = hist_stride;
+      // without a logits history the selection reads only the partials: no logits stores
+      // (10.4 MB per step at 512 rows)
+      g.Wz = fcw_pad; g.bz = fcb_pad; g.z = hist_stride ? out : nullptr; g.NZ = Vpad; g.n_valid = cfg.vocab;
+      g.hist_stride = hist_stride;
       g.part = part;
       g.Fz_hi = frag_logits.hi; g.Fz_lo = frag_logits.lo; g.Fz = frag_logits.f;
       launch_foldwide(g, stream);

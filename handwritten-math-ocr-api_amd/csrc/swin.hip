@@ -421,11 +421,20 @@ __device__ __forceinline__ floatx4 mfma3(const abf16x8& ah, const abf16x8& al, c
 // X's order; a window slot maps to its pixel through the shift roll, and a padded token's
 // k / v are the qkv bias (its LayerNorm'd input is zero, so W . 0 + b, bitwise), its
 // query is never written.  Both modes give the same bits for every real token.
+//
+// Operands come in through buffer loads (a 32-bit byte offset per lane against a
+// wave-uniform descriptor of the launch's QKV rows, qkv_bytes): a slot's row offset is
+// computed once per lane and shuffled, with no 64-bit address arithmetic, and the slots
+// without a row (>= 49, padded tokens) carry an offset past the end of the buffer, which
+// the hardware's range check turns into zeros -- no branch around any load.  A padded
+// token's k / v then take the bias (selected, bitwise the old path's value) in the
+// windows that have one (a wave-uniform ballot).  The launcher splits the batch into
+// image chunks of < 2 GiB of QKV rows.
 template <int PASSES>
 __global__ void __launch_bounds__(256) window_attention_mfma_kernel(const float* __restrict__ QKV,
                                                                     const float* __restrict__ table, RowOut out,
                                                                     int C, int heads, long npairs, WinGeom wg,
-                                                                    const float* __restrict__ bqkv) {
+                                                                    const float* __restrict__ bqkv, int qkv_bytes) {
   const int lane = threadIdx.x & 63;
   const long pair = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (pair >= npairs) return;  // whole wave; nothing below synchronises across waves
@@ -439,7 +448,10 @@ __global__ void __launch_bounds__(256) window_attention_mfma_kernel(const float*
   const int wy = win / wg.nWx;
   const int wx = win - wy * wg.nWx;
   const bool pix = bqkv != nullptr;
-  // row of window slot `lane` (slot = lane; >= 0 real token, -1 padded token, -2 slot >= 49)
+  // row of window slot `lane` (>= 0 real token, -1 padded token, -2 slot >= 49), and its
+  // byte offset: past the end of the buffer for the slots without a row (loads give 0),
+  // further past it for the padded tokens (flagged by the offset itself)
+  const unsigned oob = (unsigned)qkv_bytes, oob_pad = (unsigned)qkv_bytes + (1u << 20);
   int slot_row;
   {
     const int ty = lane / kWin;
@@ -451,26 +463,43 @@ __global__ void __launch_bounds__(256) window_attention_mfma_kernel(const float*
     slot_row = lane >= kWinTok ? -2 : (y < wg.H && x < wg.W ? (int)((b * wg.H + y) * wg.W + x) : -1);
     if (!pix) slot_row = lane < kWinTok ? (int)(win_g * kWinTok + lane) : -2;
   }
-  auto row_of = [&](int slot) { return __shfl(slot_row, slot); };
-  const float* base = QKV + h * kHeadDim;
+  const unsigned slot_off = slot_row >= 0 ? (unsigned)slot_row * (unsigned)(C3 * 4) : (slot_row == -1 ? oob_pad : oob);
+  const bool any_pad = __builtin_amdgcn_ballot_w64(slot_row == -1) != 0;  // wave-uniform
+  auto off_of = [&](int slot) { return (unsigned)__shfl((int)slot_off, slot); };
+  const __amdgpu_buffer_rsrc_t qkv = __builtin_amdgcn_make_buffer_rsrc((void*)QKV, (short)0, qkv_bytes, 0x00020000);
+  const unsigned kcol = (unsigned)(C + h * kHeadDim + 8 * g) * 4u;
+  const unsigned vcol = (unsigned)(2 * C + h * kHeadDim + l15) * 4u;
+  const unsigned qcol = (unsigned)(h * kHeadDim + 8 * g) * 4u;
+  auto ld4 = [&](unsigned off) { return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(qkv, off, 0, 0)); };
+  auto ld1 = [&](unsigned off) { return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(qkv, off, 0, 0)); };
 
+  // the bias operands of padded tokens (read only in windows that have one)
+  floatx4 kb0 = {0.f, 0.f, 0.f, 0.f}, kb1 = kb0;
+  float vb[2] = {0.f, 0.f};
+  if (any_pad) {
+    kb0 = *reinterpret_cast<const floatx4*>(bqkv + C + h * kHeadDim + 8 * g);
+    kb1 = *reinterpret_cast<const floatx4*>(bqkv + C + h * kHeadDim + 8 * g + 4);
+    vb[0] = bqkv[2 * C + h * kHeadDim + l15];
+    vb[1] = bqkv[2 * C + h * kHeadDim + 16 + l15];
+  }
   abf16x8 kh[4], kl[4];
 #pragma unroll
   for (int kt = 0; kt < 4; ++kt) {
-    const int r = row_of(16 * kt + l15);
-    const float* src = r >= 0 ? base + (size_t)r * C3 + C + 8 * g : (r == -1 ? bqkv + C + h * kHeadDim + 8 * g : nullptr);
+    const unsigned o = off_of(16 * kt + l15);
+    const floatx4 a = ld4(o + kcol);
+    const floatx4 b = ld4(o + kcol + 16);
     float x[8];
-    if (src) {
-      const floatx4 a = *reinterpret_cast<const floatx4*>(src);
-      const floatx4 b = *reinterpret_cast<const floatx4*>(src + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      x[e] = a[e];
+      x[4 + e] = b[e];
+    }
+    if (any_pad && o >= oob_pad) {  // a padded token's key is the qkv bias
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        x[e] = a[e];
-        x[4 + e] = b[e];
+        x[e] = kb0[e];
+        x[4 + e] = kb1[e];
       }
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) x[e] = 0.f;
     }
     split8(x, kh[kt], kl[kt]);
   }
@@ -484,61 +513,72 @@ __global__ void __launch_bounds__(256) window_attention_mfma_kernel(const float*
       float x[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int r = row_of(32 * s + (j >> 2) * 16 + 4 * g + (j & 3));
-        const int ch = 2 * C + 16 * dt + l15;
-        x[j] = r >= 0 ? base[(size_t)r * C3 + ch] : (r == -1 ? bqkv[h * kHeadDim + ch] : 0.f);
+        const unsigned o = off_of(32 * s + (j >> 2) * 16 + 4 * g + (j & 3));
+        x[j] = ld1(o + vcol + 64 * dt);
+        if (any_pad) x[j] = o >= oob_pad ? vb[dt] : x[j];  // a padded token's value is the qkv bias
       }
       split8(x, vh[dt][s], vl[dt][s]);
     }
 
   int type = 0;
   if (wg.sh + wg.sw > 0) type = 2 * (wy == wg.nWin / wg.nWx - 1) + (wx == wg.nWx - 1);
-  const float* tb = table + ((size_t)type * heads + h) * 64 * 64;
+  const __amdgpu_buffer_rsrc_t tbr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)table, (short)0, 4 * heads * 64 * 64 * 4, 0x00020000);
+  const unsigned tbo = (unsigned)(((type * heads + h) * 64 + l15) * 64 + 4 * g) * 4u;
 
 #pragma unroll
   for (int qt = 0; qt < 4; ++qt) {
     const int q = 16 * qt + l15;
-    const int qr = row_of(q);
+    const int qr = __shfl(slot_row, q);
     abf16x8 qh, ql;
     {
+      const unsigned o = off_of(q) + qcol;  // rows >= 49 and padded tokens read zeros (never written)
+      const floatx4 a = ld4(o);
+      const floatx4 b = ld4(o + 16);
       float x[8];
-      if (qr >= 0) {
-        const floatx4 a = *reinterpret_cast<const floatx4*>(base + (size_t)qr * C3 + 8 * g);
-        const floatx4 b = *reinterpret_cast<const floatx4*>(base + (size_t)qr * C3 + 8 * g + 4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          x[e] = a[e] * scale;
-          x[4 + e] = b[e] * scale;
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = 0.f;
+      for (int e = 0; e < 4; ++e) {
+        x[e] = a[e] * scale;
+        x[4 + e] = b[e] * scale;
       }
       split8(x, qh, ql);
     }
     floatx4 st[4];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) st[kt] = mfma3<PASSES>(kh[kt], kl[kt], qh, ql, floatx4{0.f, 0.f, 0.f, 0.f});
-    // bias + mask (+ -inf on padded keys), then softmax over the query's 64 key slots
+    // bias + mask (+ -inf on padded keys), then softmax over the query's 64 key slots.  Key
+    // tile 3 holds keys 48 + 4 g + r: only key 48 (g = 0, r = 0) exists and keys 49..63 are
+    // -inf for every real query, so r = 1..3 of that tile are skipped (exp = 0 exactly, max
+    // and sum unchanged); the padded queries' rows are never written.
+    const unsigned to = tbo + (unsigned)qt * 16u * 64u * 4u;
+    floatx4 bt[3];
+#pragma unroll
+    for (int kt = 0; kt < 3; ++kt)
+      bt[kt] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(tbr, to + 64 * kt, 0, 0));
+    const float bt3 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(tbr, to + 192, 0, 0));
     float m = -INFINITY;
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-      const floatx4 b = *reinterpret_cast<const floatx4*>(tb + q * 64 + 16 * kt + 4 * g);
+    for (int kt = 0; kt < 3; ++kt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        st[kt][r] = st[kt][r] + b[r];
+        st[kt][r] = st[kt][r] + bt[kt][r];
         m = fmaxf(m, st[kt][r]);
       }
     }
+    st[3][0] = st[3][0] + bt3;
+    m = fmaxf(m, st[3][0]);
     m = xmax16_32(m);
     float sum = 0.f;
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
+    for (int kt = 0; kt < 3; ++kt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         st[kt][r] = __expf(st[kt][r] - m);  // v_exp_f32 (libm expf: ~10 VALU each, 64 per lane)
         sum += st[kt][r];
       }
+    st[3][0] = __expf(st[3][0] - m);
+    sum += st[3][0];
+    st[3][1] = st[3][2] = st[3][3] = 0.f;
     sum = xsum16_32(sum);
     const float rs = __builtin_amdgcn_rcpf(sum);  // one rcp instead of 16 IEEE divisions
     abf16x8 ph[2], pl[2];
@@ -677,14 +717,27 @@ void launch_window_attention(const float* QKV, const float* relbias, const float
     dim3 grid((unsigned)((long)B * wg.nWin), (unsigned)heads);
     window_attention_kernel<<<grid, 256, 0, s>>>(QKV, relbias, RowOut{O, Oh, Ol}, C, wg);
   } else {
-    const long npairs = (long)B * wg.nWin * heads;
-    const unsigned blocks = (unsigned)((npairs + 3) / 4);
-    if (passes == 3)
-      window_attention_mfma_kernel<3><<<blocks, 256, 0, s>>>(QKV, relmask, RowOut{O, Oh, Ol}, C, heads, npairs, wg, bqkv);
-    else if (passes == 1)
-      window_attention_mfma_kernel<1><<<blocks, 256, 0, s>>>(QKV, relmask, RowOut{O, Oh, Ol}, C, heads, npairs, wg, bqkv);
-    else
-      throw std::runtime_error("window_attention: passes must be 0, 1 or 3");
+    if (passes != 1 && passes != 3) throw std::runtime_error("window_attention: passes must be 0, 1 or 3");
+    // the kernel addresses QKV through a buffer descriptor with 32-bit offsets: image chunks
+    // of < 2 GiB - 2 MiB of QKV rows (one chunk at every batch the bench runs)
+    const size_t rows_img = bqkv ? (size_t)wg.H * wg.W : (size_t)wg.nWin * kWinTok;
+    const size_t bytes_img = rows_img * 3 * C * sizeof(float);
+    const size_t limit = ((size_t)1 << 31) - ((size_t)2 << 20);
+    if (bytes_img > limit) throw std::runtime_error("window_attention: one image's QKV rows exceed 2 GiB");
+    const int chunk = (int)std::min<size_t>((size_t)B, limit / bytes_img);
+    for (int b0 = 0; b0 < B; b0 += chunk) {
+      const int nb = std::min(chunk, B - b0);
+      const size_t r0 = (size_t)b0 * rows_img;
+      const float* q = QKV + r0 * 3 * C;
+      const RowOut o{O ? O + r0 * C : nullptr, Oh ? Oh + r0 * C : nullptr, Ol ? Ol + r0 * C : nullptr};
+      const int nbytes = (int)((size_t)nb * bytes_img);
+      const long npairs = (long)nb * wg.nWin * heads;
+      const unsigned blocks = (unsigned)((npairs + 3) / 4);
+      if (passes == 3)
+        window_attention_mfma_kernel<3><<<blocks, 256, 0, s>>>(q, relmask, o, C, heads, npairs, wg, bqkv, nbytes);
+      else
+        window_attention_mfma_kernel<1><<<blocks, 256, 0, s>>>(q, relmask, o, C, heads, npairs, wg, bqkv, nbytes);
+    }
   }
   MOCR_HIP_CHECK(hipGetLastError());
 }

@@ -83,7 +83,9 @@ __device__ __forceinline__ void wfrag_perm(const uint16_t* hi, const uint16_t* l
 
 // timing probes of swin_attn_kernel (tools/build_variant.sh DIR -DMOCR_WATTN_PROBE=N; wrong
 // results): 1 no X loads (LN of zeros), 2 no qkv MFMAs, 3 no attention (S, softmax, PV),
-// 4 no proj MFMAs, 5 no weight loads (qkv and proj fragments from registers)
+// 4 no proj MFMAs, 5 no weight loads (qkv and proj fragments from registers), 6 weight
+// fragments loaded on even k-steps only (odd k-steps reuse them), 7 the bias + mask tile of
+// query tile 0 reused for tiles 1-3
 #ifndef MOCR_WATTN_PROBE
 #define MOCR_WATTN_PROBE 0
 #endif
@@ -202,13 +204,13 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
     for (int f = 0; f < 2; ++f)
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[f][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 w[2][2];
 #pragma unroll
     for (int ks = 0; ks < HEADS; ++ks) {
-      bf16x8 w[2][2];
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
         if constexpr (MOCR_WATTN_PROBE == 5) w[f][0] = w[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)ks, 1u, 2u, 3u});
-        else wfrag<X3>(wqh, wql, C, row0 + 16 * f + j16, 32 * ks + 8 * g, w[f]);
+        else if (MOCR_WATTN_PROBE != 6 || (ks & 1) == 0) wfrag<X3>(wqh, wql, C, row0 + 16 * f + j16, 32 * ks + 8 * g, w[f]);
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -243,13 +245,13 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
     floatx4 acc[4][2];
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[t][0] = acc[t][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 w[2][2];
 #pragma unroll
     for (int ks = 0; ks < HEADS; ++ks) {
-      bf16x8 w[2][2];
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
         if constexpr (MOCR_WATTN_PROBE == 5) w[f][0] = w[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)ks, 1u, 2u, 3u});
-        else wfrag<X3>(wqh, wql, C, 2 * C + 32 * h + 16 * f + j16, 32 * ks + 8 * g, w[f]);
+        else if (MOCR_WATTN_PROBE != 6 || (ks & 1) == 0) wfrag<X3>(wqh, wql, C, 2 * C + 32 * h + 16 * f + j16, 32 * ks + 8 * g, w[f]);
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -297,15 +299,22 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
   int type = 0;
   if (wg.sh + wg.sw > 0) type = 2 * (wy == wg.nWin / wg.nWx - 1) + (wx == wg.nWx - 1);
   const float* tb = p.table + ((size_t)type * HEADS + h) * 64 * 64;
-  floatx4 bm[4];  // bias + mask of the current query tile
+  // bias + mask of the current query tile.  Key tile 3 holds keys 48 + 4 g + r: only key 48
+  // (g = 0, r = 0) exists, keys 49..63 are -inf for every real query (build_relmask), so
+  // r = 1..3 of that tile are skipped (exp = 0 exactly; max and sum unchanged) and only r = 0
+  // of its bias is loaded.  The padded queries 49..63 change, but their rows are never stored.
+  floatx4 bm[3];
+  float bm3;
 #pragma unroll
-  for (int kt = 0; kt < 4; ++kt) bm[kt] = *reinterpret_cast<const floatx4*>(tb + j16 * 64 + 16 * kt + 4 * g);
+  for (int kt = 0; kt < 3; ++kt) bm[kt] = *reinterpret_cast<const floatx4*>(tb + j16 * 64 + 16 * kt + 4 * g);
+  bm3 = tb[j16 * 64 + 48 + 4 * g];
 #pragma unroll
   for (int qt = 0; qt < 4; ++qt) {
-    if (qt > 0) {
+    if (qt > 0 && MOCR_WATTN_PROBE != 7) {
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
+      for (int kt = 0; kt < 3; ++kt)
         bm[kt] = *reinterpret_cast<const floatx4*>(tb + (16 * qt + j16) * 64 + 16 * kt + 4 * g);
+      bm3 = tb[(16 * qt + j16) * 64 + 48 + 4 * g];
     }
     if constexpr (MOCR_WATTN_PROBE == 3) {
       const int off = ((qt * HEADS + h) * 64 + lane) * 16;
@@ -318,22 +327,27 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
     for (int kt = 0; kt < 4; ++kt) st[kt] = mma<X3>(kf[kt], qf4[qt], floatx4{0.f, 0.f, 0.f, 0.f});
     float m = -INFINITY;
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
+    for (int kt = 0; kt < 3; ++kt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         st[kt][r] = st[kt][r] + bm[kt][r];
         m = fmaxf(m, st[kt][r]);
       }
     }
+    st[3][0] = st[3][0] + bm3;
+    m = fmaxf(m, st[3][0]);
     m = xmax16_32(m);
     float sum = 0.f;
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
+    for (int kt = 0; kt < 3; ++kt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         st[kt][r] = __expf(st[kt][r] - m);
         sum += st[kt][r];
       }
+    st[3][0] = __expf(st[3][0] - m);
+    sum += st[3][0];
+    st[3][1] = st[3][2] = st[3][3] = 0.f;
     sum = xsum16_32(sum);
     bf16x8 pf[2][2];
 #pragma unroll
@@ -384,13 +398,13 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
 #pragma unroll
   for (int t = 0; t < 4; ++t) ap[0][t] = ap[1][t] = floatx4{0.f, 0.f, 0.f, 0.f};
   __builtin_amdgcn_s_setprio(1);
+  bf16x8 wa[2][2];
 #pragma unroll
   for (int hh = 0; hh < HEADS; ++hh) {
-    bf16x8 wa[2][2];
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
       if constexpr (MOCR_WATTN_PROBE == 5) wa[f][0] = wa[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)hh, 1u, 2u, 3u});
-      else wfrag_perm<X3>(wph, wpl, C, 32 * h + 16 * f + j16, 32 * hh + 4 * g, wa[f]);
+      else if (MOCR_WATTN_PROBE != 6 || (hh & 1) == 0) wfrag_perm<X3>(wph, wpl, C, 32 * h + 16 * f + j16, 32 * hh + 4 * g, wa[f]);
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -622,7 +636,7 @@ swin_attn_noproj_kernel(SwinAttnParams p) {
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
         if constexpr (MOCR_WATTN_PROBE == 5) w[f][0] = w[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)ks, 1u, 2u, 3u});
-        else wfrag<X3>(wqh, wql, C, row0 + 16 * f + j16, 32 * ks + 8 * g, w[f]);
+        else if (MOCR_WATTN_PROBE != 6 || (ks & 1) == 0) wfrag<X3>(wqh, wql, C, row0 + 16 * f + j16, 32 * ks + 8 * g, w[f]);
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
