@@ -458,8 +458,11 @@ __global__ void __launch_bounds__(64 * NW) foldwide_kernel(FoldGemmParams p) {
 // Fragment-major copy of a row-major [N, K] fp32 weight (N % 16 == 0, K % 32 == 0):
 // X3 planes hi / lo [N/16][K/32][64 lanes][8] (bf16 split as split2_bf16), or fp32
 // [N/16][K/16][64 lanes][4]; lane L holds W[16 j + (L & 15)][k0 + (8 or 4) (L >> 4) + e].
+// perm (planes only): lane L's 8 elements are k0 + 4 (L >> 4) + {0..3, 16..19}, the
+// permuted k order of wattn.hip's proj GEMM (its B fragments are the attention's O^T
+// accumulators of two 16-dim tiles).
 __global__ void frag_pack_kernel(const float* __restrict__ W, int N, int K, uint16_t* __restrict__ hi,
-                                 uint16_t* __restrict__ lo, float* __restrict__ f32) {
+                                 uint16_t* __restrict__ lo, float* __restrict__ f32, int perm) {
   const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // one lane-chunk
   const bool x3 = hi != nullptr;
   const int ks = x3 ? 32 : 16, per = x3 ? 8 : 4;
@@ -469,11 +472,14 @@ __global__ void frag_pack_kernel(const float* __restrict__ W, int N, int K, uint
   const size_t t = idx / 64;
   const int s = t % (K / ks);
   const int j = t / (K / ks);
-  const float* src = W + (size_t)(16 * j + (L & 15)) * K + s * ks + per * (L >> 4);
+  const float* src = W + (size_t)(16 * j + (L & 15)) * K + s * ks + (perm ? 4 : per) * (L >> 4);
   if (x3) {
     uint32_t h[4], l[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) split2_bf16(src[2 * e], src[2 * e + 1], h[e], l[e]);
+    for (int e = 0; e < 4; ++e) {
+      const int k0 = perm && e >= 2 ? 12 : 0;  // elements 4..7 at +16 under perm
+      split2_bf16(src[k0 + 2 * e], src[k0 + 2 * e + 1], h[e], l[e]);
+    }
     reinterpret_cast<uint4*>(hi)[idx] = make_uint4(h[0], h[1], h[2], h[3]);
     reinterpret_cast<uint4*>(lo)[idx] = make_uint4(l[0], l[1], l[2], l[3]);
   } else {
@@ -604,10 +610,12 @@ extern "C" int mocr_debug_fold_ts(unsigned long long* out, int n) {
 }
 #endif
 
-void launch_frag_pack(const float* W, int N, int K, uint16_t* hi, uint16_t* lo, float* f32, hipStream_t s) {
+void launch_frag_pack(const float* W, int N, int K, uint16_t* hi, uint16_t* lo, float* f32, hipStream_t s,
+                      bool perm) {
   if (N % 16 != 0 || K % 32 != 0 || (!hi != !lo) || (!hi && !f32)) throw std::runtime_error("frag_pack: N % 16, K % 32");
+  if (perm && !hi) throw std::runtime_error("frag_pack: the permuted k order is built for bf16 planes");
   const size_t chunks = (size_t)N * K / (hi ? 8 : 4);
-  frag_pack_kernel<<<(unsigned)((chunks + 255) / 256), 256, 0, s>>>(W, N, K, hi, lo, f32);
+  frag_pack_kernel<<<(unsigned)((chunks + 255) / 256), 256, 0, s>>>(W, N, K, hi, lo, f32, perm ? 1 : 0);
   MOCR_HIP_CHECK(hipGetLastError());
 }
 

@@ -363,6 +363,9 @@ struct mocr_engine {
   };
   std::vector<std::array<FragW, 6>> fragw;
   FragW frag_logits;
+  // wattn.hip swin_attn_kernel: fragment-major W_qkv and (permuted k order) W_proj of the
+  // stage-1/2 blocks, bf16 hi / lo planes
+  std::vector<std::array<FragW, 2>> swinfrag;
   std::vector<void*> frag_allocs;
 
   // timing
@@ -918,6 +921,7 @@ struct mocr_engine {
       launch_split_bf16(kvw_all, kvwh, kvwl, (size_t)cfg.n_layers * 2 * d * d, stream);
       MOCR_HIP_CHECK(hipStreamSynchronize(stream));
     }
+    if (dwh && cfg.arch != MOCR_ARCH_RES18TRANS) pack_swin_frags();
     if (fold_greedy()) fold_decoder();
     if (fold_wide()) pack_frags();
     MOCR_HIP_CHECK(hipDeviceSynchronize());
@@ -983,6 +987,30 @@ struct mocr_engine {
       frag_allocs.push_back(f.f);
     }
     launch_frag_pack(W, N, K, f.hi, f.lo, f.f, stream);
+  }
+  void pack_swin_frags() {
+    int nb = 0;
+    for (int st = 0; st < kStages; ++st)
+      if (swin_attn_fused_supported(stage[st].C)) nb += kDepth[st];
+    if (swinfrag.empty()) swinfrag.resize(nb);
+    for (int st = 0, bi = 0; st < kStages; ++st) {
+      const int C = stage[st].C;
+      if (!swin_attn_fused_supported(C)) break;  // stages 1-2 only (C = 96, 192)
+      for (int j = 0; j < kDepth[st]; ++j, ++bi) {
+        const SwinBlockW& w = lay->blocks[bi];
+        for (int m = 0; m < 2; ++m) {
+          FragW& f = swinfrag[bi][m];
+          const int N = m == 0 ? 3 * C : C;
+          if (!f.hi) {
+            f.hi = dalloc<uint16_t>((size_t)N * C);
+            f.lo = dalloc<uint16_t>((size_t)N * C);
+            frag_allocs.push_back(f.hi);
+            frag_allocs.push_back(f.lo);
+          }
+          launch_frag_pack(W(m == 0 ? w.qkvw : w.projw), N, C, f.hi, f.lo, nullptr, stream, m == 1);
+        }
+      }
+    }
   }
   void pack_frags() {
     const int d = cfg.d_model, ff = cfg.d_ff, L = cfg.n_layers;
@@ -1240,6 +1268,10 @@ struct mocr_engine {
           ap.bqkv = W(w.qkvb);
           ap.wproj = dwh + w.projw;
           ap.wproj_lo = dwl ? dwl + w.projw : nullptr;
+          ap.wqkv_fm = swinfrag.at(bi)[0].hi;
+          ap.wqkv_fm_lo = dwl ? swinfrag[bi][0].lo : nullptr;
+          ap.wproj_fm = swinfrag[bi][1].hi;
+          ap.wproj_fm_lo = dwl ? swinfrag[bi][1].lo : nullptr;
           ap.bproj = W(w.projb);
           ap.table = relmask[bi];
           ap.B = B;

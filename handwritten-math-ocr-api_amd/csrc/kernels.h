@@ -154,6 +154,10 @@ struct SwinAttnParams {
   const float* bqkv;          // [3C]
   const void *wproj, *wproj_lo;  // [C, C]
   const float* bproj;         // [C]
+  // the fused stage-1/2 kernel (launch_swin_attn_fused): the same weights fragment-major
+  // (launch_frag_pack: one contiguous 1-KB load per 16-row x 32-k fragment and plane),
+  // proj in its permuted k order
+  const void *wqkv_fm, *wqkv_fm_lo, *wproj_fm, *wproj_fm_lo;
   const float* table;         // [4 window types][heads][64 q][64 key] bias + mask (build_relmask)
   uint16_t *att_hi, *att_lo;  // noproj: O planes [B * nWin * 49, C] (window-token rows), or
                               // att_pixel_rows: [B * H * W, C] in X's row order, padding dropped
@@ -262,7 +266,8 @@ void launch_foldgemm(const FoldGemmParams& p, hipStream_t s);
 void launch_foldwide(const FoldGemmParams& p, hipStream_t s);
 // Fragment-major copy of a row-major [N, K] fp32 weight for launch_foldwide: bf16x3 hi / lo
 // planes (hi, lo non-null) or fp32 (f32).  N % 16 == 0, K % 32 == 0.
-void launch_frag_pack(const float* W, int N, int K, uint16_t* hi, uint16_t* lo, float* f32, hipStream_t s);
+void launch_frag_pack(const float* W, int N, int K, uint16_t* hi, uint16_t* lo, float* f32, hipStream_t s,
+                      bool perm = false);
 
 // Attention of the newest position with folded inputs, one workgroup per (row, head):
 // q = rstd (z_q - mu s) + c from z [B, z_ld] and z_stats (plain z when z_stats is null).

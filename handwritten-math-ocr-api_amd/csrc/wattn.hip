@@ -66,21 +66,6 @@ __device__ __forceinline__ void wfrag(const uint16_t* hi, const uint16_t* lo, in
   if constexpr (X3) f[1] = *reinterpret_cast<const bf16x8*>(lo + o);
 }
 
-// channels {ch .. ch+3, ch+16 .. ch+19} of row `row` (proj's permuted k order)
-template <bool X3>
-__device__ __forceinline__ void wfrag_perm(const uint16_t* hi, const uint16_t* lo, int C, int row, int ch,
-                                           bf16x8 (&f)[2]) {
-  const size_t o = (size_t)row * C + ch;
-  const uint2 a = *reinterpret_cast<const uint2*>(hi + o);
-  const uint2 b = *reinterpret_cast<const uint2*>(hi + o + 16);
-  f[0] = __builtin_bit_cast(bf16x8, make_uint4(a.x, a.y, b.x, b.y));
-  if constexpr (X3) {
-    const uint2 c = *reinterpret_cast<const uint2*>(lo + o);
-    const uint2 d = *reinterpret_cast<const uint2*>(lo + o + 16);
-    f[1] = __builtin_bit_cast(bf16x8, make_uint4(c.x, c.y, d.x, d.y));
-  }
-}
-
 // timing probes of swin_attn_kernel (tools/build_variant.sh DIR -DMOCR_WATTN_PROBE=N; wrong
 // results): 1 no X loads (LN of zeros), 2 no qkv MFMAs, 3 no attention (S, softmax, PV),
 // 4 no proj MFMAs, 5 no weight loads (qkv and proj fragments from registers), 6 weight
@@ -188,8 +173,14 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
 
   // ---- B: k^T, v, q^T of head h, one 8-tile GEMM at a time (each converted to its
   // attention fragments at once, so only one set of accumulators is live)
-  const uint16_t* wqh = static_cast<const uint16_t*>(p.wqkv);
-  const uint16_t* wql = static_cast<const uint16_t*>(p.wqkv_lo);
+  // W_qkv fragment-major (launch_frag_pack): fragment (16-row tile, k-step) = 64 lanes x 16 B
+  const bf16x8* wqh = static_cast<const bf16x8*>(p.wqkv_fm);
+  const bf16x8* wql = static_cast<const bf16x8*>(p.wqkv_fm_lo);
+  auto wfm = [&](int row0, int f, int ks, bf16x8(&w)[2]) {
+    const int o = (((row0 >> 4) + f) * HEADS + ks) * 64 + lane;
+    w[0] = wqh[o];
+    if constexpr (X3) w[1] = wql[o];
+  };
   const float* bq = p.bqkv;
   // LN fragment (tokens 16t + j16, channels 32ks + 8g ..): B of the k^T / q^T GEMMs, A of v's
   auto xfrag = [&](int ks, int t, bf16x8(&f)[2]) {
@@ -210,7 +201,7 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
         if constexpr (MOCR_WATTN_PROBE == 5) w[f][0] = w[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)ks, 1u, 2u, 3u});
-        else if (MOCR_WATTN_PROBE != 6 || (ks & 1) == 0) wfrag<X3>(wqh, wql, C, row0 + 16 * f + j16, 32 * ks + 8 * g, w[f]);
+        else if (MOCR_WATTN_PROBE != 6 || (ks & 1) == 0) wfm(row0, f, ks, w[f]);
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -251,7 +242,7 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
         if constexpr (MOCR_WATTN_PROBE == 5) w[f][0] = w[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)ks, 1u, 2u, 3u});
-        else if (MOCR_WATTN_PROBE != 6 || (ks & 1) == 0) wfrag<X3>(wqh, wql, C, 2 * C + 32 * h + 16 * f + j16, 32 * ks + 8 * g, w[f]);
+        else if (MOCR_WATTN_PROBE != 6 || (ks & 1) == 0) wfm(2 * C + 32 * h, f, ks, w[f]);
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -382,8 +373,10 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
   __syncthreads();
 
   // ---- D: out^T rows 32h .. 32h+31 = W_proj . O^T, + bias + residual
-  const uint16_t* wph = static_cast<const uint16_t*>(p.wproj);
-  const uint16_t* wpl = static_cast<const uint16_t*>(p.wproj_lo);
+  // W_proj fragment-major in the permuted k order (launch_frag_pack perm): lane (g, j) of
+  // fragment (16-row tile, head hh) holds channels 32 hh + {4g..4g+3, 16+4g..16+4g+3}
+  const bf16x8* wph = static_cast<const bf16x8*>(p.wproj_fm);
+  const bf16x8* wpl = static_cast<const bf16x8*>(p.wproj_fm_lo);
   long pxo[4];
   floatx4 xres[2][4];  // the residual rows, loaded before the GEMM
 #pragma unroll
@@ -404,7 +397,11 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
       if constexpr (MOCR_WATTN_PROBE == 5) wa[f][0] = wa[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)hh, 1u, 2u, 3u});
-      else if (MOCR_WATTN_PROBE != 6 || (hh & 1) == 0) wfrag_perm<X3>(wph, wpl, C, 32 * h + 16 * f + j16, 32 * hh + 4 * g, wa[f]);
+      else if (MOCR_WATTN_PROBE != 6 || (hh & 1) == 0) {
+        const int o = ((2 * h + f) * HEADS + hh) * 64 + lane;
+        wa[f][0] = wph[o];
+        if constexpr (X3) wa[f][1] = wpl[o];
+      }
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -970,6 +967,8 @@ void launch_swin_attn_fused(const SwinAttnParams& p, hipStream_t s) {
   if (p.B <= 0) return;
   if ((p.wqkv_lo == nullptr) != (p.wproj_lo == nullptr))
     throw std::runtime_error("swin_attn: lo planes for both or neither");
+  if (!p.wqkv_fm || !p.wproj_fm || (p.wqkv_lo && (!p.wqkv_fm_lo || !p.wproj_fm_lo)))
+    throw std::runtime_error("swin_attn: fragment-major weights (launch_frag_pack) missing");
   if (p.heads * 32 != p.C) throw std::runtime_error("swin_attn: head dim must be 32");
   switch (p.C) {
     case 96: launch_c<96, 3>(p, s); break;
