@@ -366,6 +366,7 @@ struct mocr_engine {
   // wattn.hip swin_attn_kernel: fragment-major W_qkv and (permuted k order) W_proj of the
   // stage-1/2 blocks, bf16 hi / lo planes
   std::vector<std::array<FragW, 2>> swinfrag;
+  std::vector<void*> mlppack;  // mlp.hip: the stage-1/2 MLP kernel's W1 | W2 chunk images per block
   std::vector<void*> frag_allocs;
 
   // timing
@@ -991,14 +992,14 @@ struct mocr_engine {
   void pack_swin_frags() {
     int nb = 0;
     for (int st = 0; st < kStages; ++st)
-      if (swin_attn_fused_supported(stage[st].C)) nb += kDepth[st];
+      if (stage[st].C <= 384) nb += kDepth[st];
     if (swinfrag.empty()) swinfrag.resize(nb);
     for (int st = 0, bi = 0; st < kStages; ++st) {
       const int C = stage[st].C;
-      if (!swin_attn_fused_supported(C)) break;  // stages 1-2 only (C = 96, 192)
+      if (C > 384) break;  // stages 1-3: the fused kernels' W_qkv (+ W_proj at C = 96, 192)
       for (int j = 0; j < kDepth[st]; ++j, ++bi) {
         const SwinBlockW& w = lay->blocks[bi];
-        for (int m = 0; m < 2; ++m) {
+        for (int m = 0; m < (swin_attn_fused_supported(C) ? 2 : 1); ++m) {
           FragW& f = swinfrag[bi][m];
           const int N = m == 0 ? 3 * C : C;
           if (!f.hi) {
@@ -1008,6 +1009,20 @@ struct mocr_engine {
             frag_allocs.push_back(f.lo);
           }
           launch_frag_pack(W(m == 0 ? w.qkvw : w.projw), N, C, f.hi, f.lo, nullptr, stream, m == 1);
+        }
+        if (const size_t pb = mlp_pack_bytes(C, dwl != nullptr)) {
+          if (mlppack.size() <= (size_t)bi) mlppack.resize(bi + 1, nullptr);
+          if (!mlppack[bi]) {
+            mlppack[bi] = dalloc<char>(pb);
+            frag_allocs.push_back(mlppack[bi]);
+          }
+          MlpParams mp{};
+          mp.C = C;
+          mp.w1 = dwh + w.fc1w;
+          mp.w1lo = dwl ? dwl + w.fc1w : nullptr;
+          mp.w2 = dwh + w.fc2w;
+          mp.w2lo = dwl ? dwl + w.fc2w : nullptr;
+          launch_mlp_pack(mp, mlppack[bi], stream);
         }
       }
     }
@@ -1288,6 +1303,10 @@ struct mocr_engine {
           ap.ln_b = W(w.n1b);
           ap.wqkv = dwh + w.qkvw;
           ap.wqkv_lo = dwl ? dwl + w.qkvw : nullptr;
+          if (C == 384) {
+            ap.wqkv_fm = swinfrag.at(bi)[0].hi;
+            ap.wqkv_fm_lo = dwl ? swinfrag[bi][0].lo : nullptr;
+          }
           ap.bqkv = W(w.qkvb);
           ap.table = relmask[bi];
           ap.att_hi = ATTh;
@@ -1352,6 +1371,7 @@ struct mocr_engine {
           mp.w2 = dwh + w.fc2w;
           mp.w2lo = dwl ? dwl + w.fc2w : nullptr;
           mp.b2 = W(w.fc2b);
+          mp.wpack = bi < (int)mlppack.size() ? mlppack[bi] : nullptr;
           timed(mlp_n[s], 16.0 * rows * C * C, 8.0 * rows * C + (dwl ? 4.0 : 2.0) * 8.0 * C * C,
                 [&] { launch_mlp_fused(mp, stream); });
         } else {

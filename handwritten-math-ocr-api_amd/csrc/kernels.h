@@ -123,9 +123,15 @@ struct MlpParams {
   const float* b1;          // [4C]
   const void *w2, *w2lo;    // [C, 4C]
   const float* b2;          // [C]
+  const void* wpack;        // C = 96, 192: W1 | W2 as the kernel's LDS chunk images (launch_mlp_pack)
 };
 bool mlp_fused_supported(int C);
 void launch_mlp_fused(const MlpParams& p, hipStream_t s);
+// The stage-1/2 MLP kernel's weight chunks in its LDS image order (swizzled, GEMM 2's
+// permuted k order), packed once at load from w1 / w2 (/ lo) so that each 1-KB piece is one
+// contiguous 16-B-per-lane load: mlp_pack_bytes(C, x3) bytes at `out`.
+size_t mlp_pack_bytes(int C, bool x3);
+void launch_mlp_pack(const MlpParams& p, void* out, hipStream_t s);
 
 // out = LayerNorm(X) W^T + b at C = 384 (mlp.hip lngemm384_kernel): stage 3's norm1 + qkv
 // over the image tokens at >= 128 images, and merge 1 (PatchMerging of the 96-channel
@@ -154,7 +160,8 @@ struct SwinAttnParams {
   const float* bqkv;          // [3C]
   const void *wproj, *wproj_lo;  // [C, C]
   const float* bproj;         // [C]
-  // the fused stage-1/2 kernel (launch_swin_attn_fused): the same weights fragment-major
+  // the fused stage-1/2 kernel (launch_swin_attn_fused) and the stage-3 no-proj kernel
+  // (launch_swin_attn_noproj at C = 384, W_qkv only): the same weights fragment-major
   // (launch_frag_pack: one contiguous 1-KB load per 16-row x 32-k fragment and plane),
   // proj in its permuted k order
   const void *wqkv_fm, *wqkv_fm_lo, *wproj_fm, *wproj_fm_lo;

@@ -154,10 +154,13 @@ __global__ void __launch_bounds__(512) mlp_fused_kernel(MlpParams p) {
   constexpr int NST = NPIECE / 8;
   constexpr int KPL = (DMA1 + DMA2) / 8;  // pieces per wave per plane
   static_assert(KPL * 8 == DMA1 + DMA2, "pieces per wave");
+  // piece k of chunk jc from the packed chunk images (launch_mlp_pack: the LDS bytes in order)
+  const char* wpk = static_cast<const char*>(p.wpack);
+  auto piece = [&](int jc, int k) {
+    return *reinterpret_cast<const uint4*>(wpk + (size_t)jc * BUF + mlp_piece_dst<PL, DMA1, KPL, W1B, W2B>(k, wave, lane));
+  };
   StgList<0, NST> stg;
-  stg.load([&](int k) {
-    return mlp_piece_load<C, NC, PL, DMA1, KPL, RC, SW1, SH1, RB, SH2>(p, 0, k, wave, lane);
-  });
+  stg.load([&](int k) { return piece(0, k); });
   for (int i = tid; i < HID; i += 512) b1s[i] = p.b1[i];
   for (int i = tid; i < C; i += 512) b2s[i] = p.b2[i];
 
@@ -228,9 +231,7 @@ __global__ void __launch_bounds__(512) mlp_fused_kernel(MlpParams p) {
   for (int jc = 0; jc < NCH; ++jc) {
     const bool more = jc + 1 < NCH;
     if (more) {
-      stg.load([&](int k) {
-        return mlp_piece_load<C, NC, PL, DMA1, KPL, RC, SW1, SH1, RB, SH2>(p, jc + 1, k, wave, lane);
-      });
+      stg.load([&](int k) { return piece(jc + 1, k); });
     }
     const char* w1s = lds + (jc & 1) * BUF;
     const char* w2s = w1s + PL * W1B;
@@ -887,6 +888,38 @@ __global__ void __launch_bounds__(256) lngemm384_kernel(LnGemm384Params p) {
   }
 }
 
+// mlp_fused_kernel<C, TT, NC, PASSES>'s chunk images: chunk jc at jc * BUF, piece k of wave w
+// at the LDS offset the kernel stores it to, holding what mlp_piece_load gathers for it.
+template <int C, int NC, int PASSES>
+struct MlpImage {
+  static constexpr int PL = PASSES == 3 ? 2 : 1, RC = C / 8;
+  static constexpr int SW1 = (RC % 16 == 0) ? 16 : ((RC % 8 == 0) ? 8 : 4), SH1 = SW1 == 16 ? 0 : 1;
+  static constexpr int RB = NC / 8, SH2 = RB == 4 ? 1 : 0;
+  static constexpr int W1B = NC * C * 2, W2B = C * NC * 2, DMA1 = W1B / 1024, DMA2 = W2B / 1024;
+  static constexpr int KPL = (DMA1 + DMA2) / 8, NST = PL * KPL, BUF = PL * (W1B + W2B), NCH = 4 * C / NC;
+};
+template <int C, int NC, int PASSES>
+__global__ void mlp_pack_kernel(MlpParams p, char* __restrict__ out) {
+  using I = MlpImage<C, NC, PASSES>;
+  const int lane = threadIdx.x & 63;
+  const int wave = (threadIdx.x >> 6) & 7;
+  const int k = blockIdx.x % I::NST;
+  const int jc = blockIdx.x / I::NST;
+  const uint4 v = mlp_piece_load<C, NC, I::PL, I::DMA1, I::KPL, I::RC, I::SW1, I::SH1, I::RB, I::SH2>(p, jc, k, wave, lane);
+  *reinterpret_cast<uint4*>(out + (size_t)jc * I::BUF +
+                            mlp_piece_dst<I::PL, I::DMA1, I::KPL, I::W1B, I::W2B>(k, wave, lane)) = v;
+}
+template <int C, int NC>
+void launch_pack_c(const MlpParams& p, void* out, hipStream_t s) {
+  if (p.w1lo) {
+    using I = MlpImage<C, NC, 3>;
+    mlp_pack_kernel<C, NC, 3><<<I::NCH * I::NST, 512, 0, s>>>(p, static_cast<char*>(out));
+  } else {
+    using I = MlpImage<C, NC, 1>;
+    mlp_pack_kernel<C, NC, 1><<<I::NCH * I::NST, 512, 0, s>>>(p, static_cast<char*>(out));
+  }
+}
+
 template <int C, int TT, int NC>
 void launch_mlp_c(const MlpParams& p, hipStream_t s) {
   const unsigned grid = (unsigned)((p.M + 128 * TT - 1) / (128 * TT));
@@ -921,13 +954,31 @@ void launch_lngemm384(const LnGemm384Params& p, hipStream_t s) {
   MOCR_HIP_CHECK(hipGetLastError());
 }
 
+// hidden chunk NC per C as launch_mlp_fused runs the kernel
+size_t mlp_pack_bytes(int C, bool x3) {
+  if (C != 96 && C != 192) return 0;
+  return (size_t)(x3 ? 2 : 1) * 4 * C * C * 2 * 2;  // NCH chunks x BUF = PL x (W1 + W2) bf16
+}
+
+void launch_mlp_pack(const MlpParams& p, void* out, hipStream_t s) {
+  if ((p.w1lo == nullptr) != (p.w2lo == nullptr) || !p.w1 || !p.w2 || !out)
+    throw std::runtime_error("mlp_pack: planes");
+  switch (p.C) {
+    case 96: launch_pack_c<96, 64>(p, out, s); break;
+    case 192: launch_pack_c<192, 32>(p, out, s); break;
+    default: throw std::runtime_error("mlp_pack: built for C = 96, 192");
+  }
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
 void launch_mlp_fused(const MlpParams& p, hipStream_t s) {
   if (p.M <= 0) return;
   if ((p.w1lo == nullptr) != (p.w2lo == nullptr)) throw std::runtime_error("mlp: lo planes for both or neither");
+  if ((p.C == 96 || p.C == 192) && !p.wpack) throw std::runtime_error("mlp: packed chunk images (launch_mlp_pack) missing");
   switch (p.C) {
     // rows per wave 16 TT and hidden chunk NC measured best (TT = 1 at C = 96: 514 vs 420 us
     // per s1 block; TT = 2 at C = 192 spills)
-    case 96: launch_mlp_c<96, 2, 64>(p, s); break;
+    case 96: launch_mlp_c<96, 2, 64>(p, s); break;  // NC: launch_mlp_pack's chunks
     case 192: launch_mlp_c<192, 1, 32>(p, s); break;
     case 384: {
       const unsigned grid = (unsigned)((p.M + 127) / 128);

@@ -611,8 +611,14 @@ swin_attn_noproj_kernel(SwinAttnParams p) {
   // ---- B-C per head: k^T, v, q^T of head h, one 8-tile GEMM at a time (each converted
   // to its attention fragments at once, so only one set of accumulators is live), then
   // attention per 16-query tile
-  const uint16_t* wqh = static_cast<const uint16_t*>(p.wqkv);
-  const uint16_t* wql = static_cast<const uint16_t*>(p.wqkv_lo);
+  // W_qkv fragment-major (launch_frag_pack), as swin_attn_kernel
+  const bf16x8* wqh = static_cast<const bf16x8*>(p.wqkv_fm);
+  const bf16x8* wql = static_cast<const bf16x8*>(p.wqkv_fm_lo);
+  auto wfm = [&](int row0, int f, int ks, bf16x8(&w)[2]) {
+    const int o = (((row0 >> 4) + f) * HEADS + ks) * 64 + lane;
+    w[0] = wqh[o];
+    if constexpr (X3) w[1] = wql[o];
+  };
   const float* bq = p.bqkv;
   // LN fragment (tokens 16t + j16, channels 32ks + 8g ..): B of the k^T / q^T GEMMs, A of v's
   auto xfrag = [&](int ks, int t, bf16x8(&f)[2]) {
@@ -633,7 +639,7 @@ swin_attn_noproj_kernel(SwinAttnParams p) {
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
         if constexpr (MOCR_WATTN_PROBE == 5) w[f][0] = w[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)ks, 1u, 2u, 3u});
-        else if (MOCR_WATTN_PROBE != 6 || (ks & 1) == 0) wfrag<X3>(wqh, wql, C, row0 + 16 * f + j16, 32 * ks + 8 * g, w[f]);
+        else if (MOCR_WATTN_PROBE != 6 || (ks & 1) == 0) wfm(row0, f, ks, w[f]);
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -681,7 +687,7 @@ swin_attn_noproj_kernel(SwinAttnParams p) {
       for (int ks = 0; ks < HEADS; ++ks) {
         bf16x8 w[2][2];
 #pragma unroll
-        for (int f = 0; f < 2; ++f) wfrag<X3>(wqh, wql, C, 2 * C + 32 * h + 16 * f + j16, 32 * ks + 8 * g, w[f]);
+        for (int f = 0; f < 2; ++f) wfm(2 * C + 32 * h, f, ks, w[f]);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           bf16x8 xf[2];
@@ -994,6 +1000,8 @@ void launch_swin_attn_noproj(const SwinAttnParams& p, hipStream_t s) {
     MOCR_HIP_CHECK(hipGetLastError());
     return;
   }
+  if (!p.wqkv_fm || (p.wqkv_lo && !p.wqkv_fm_lo))
+    throw std::runtime_error("swin_attn_noproj: fragment-major W_qkv (launch_frag_pack) missing");
   // 12 waves (one head each, 3 per SIMD, 166 VGPRs) and k-steps unrolled by 2: 285 us per
   // s3 block at B=64, 384² vs 313 (8 waves over the 12 heads, 2 per SIMD), 302 (8 waves,
   // unroll 4), 318 (8 waves, no unroll)
