@@ -366,7 +366,9 @@ struct mocr_engine {
   // wattn.hip swin_attn_kernel: fragment-major W_qkv and (permuted k order) W_proj of the
   // stage-1/2 blocks, bf16 hi / lo planes
   std::vector<std::array<FragW, 2>> swinfrag;
-  std::vector<void*> mlppack;  // mlp.hip: the stage-1/2 MLP kernel's W1 | W2 chunk images per block
+  std::vector<void*> mlppack;  // mlp.hip: the fused MLP kernels' W1 | W2 chunk images per block
+  std::vector<void*> lngpack;  // mlp.hip: lngemm384's W_qkv chunk images per stage-3 block
+  void* mergepack = nullptr;   // and of merge 1's reduction
   std::vector<void*> frag_allocs;
 
   // timing
@@ -990,6 +992,14 @@ struct mocr_engine {
     launch_frag_pack(W, N, K, f.hi, f.lo, f.f, stream);
   }
   void pack_swin_frags() {
+    {  // merge 1: 4 x 96 = 384 channels -> 192 (lngemm384)
+      const MergeW& m = lay->merge[0];
+      if (!mergepack) {
+        mergepack = dalloc<char>((size_t)192 * 384 * 2 * (dwl ? 2 : 1));
+        frag_allocs.push_back(mergepack);
+      }
+      launch_lngemm384_pack(dwh + m.redw, dwl ? dwl + m.redw : nullptr, 192, mergepack, stream);
+    }
     int nb = 0;
     for (int st = 0; st < kStages; ++st)
       if (stage[st].C <= 384) nb += kDepth[st];
@@ -1023,6 +1033,14 @@ struct mocr_engine {
           mp.w2 = dwh + w.fc2w;
           mp.w2lo = dwl ? dwl + w.fc2w : nullptr;
           launch_mlp_pack(mp, mlppack[bi], stream);
+        }
+        if (C == 384) {
+          if (lngpack.size() <= (size_t)bi) lngpack.resize(bi + 1, nullptr);
+          if (!lngpack[bi]) {
+            lngpack[bi] = dalloc<char>((size_t)3 * C * C * 2 * (dwl ? 2 : 1));
+            frag_allocs.push_back(lngpack[bi]);
+          }
+          launch_lngemm384_pack(dwh + w.qkvw, dwl ? dwl + w.qkvw : nullptr, 3 * C, lngpack[bi], stream);
         }
       }
     }
@@ -1330,6 +1348,7 @@ struct mocr_engine {
             LnGemm384Params lp{};
             lp.X = X; lp.M = rows; lp.ln_g = W(w.n1w); lp.ln_b = W(w.n1b);
             lp.w = dwh + w.qkvw; lp.wlo = dwl ? dwl + w.qkvw : nullptr; lp.b = W(w.qkvb);
+            lp.wpk = lngpack.at(bi);
             lp.out = QKV; lp.N = 3 * C;
             timed(lnqkv_n[s], 6.0 * rows * C * C, 4.0 * rows * C + 12.0 * rows * C + (dwl ? 4.0 : 2.0) * 3.0 * C * C,
                   [&] { launch_lngemm384(lp, stream); });
@@ -1392,6 +1411,7 @@ struct mocr_engine {
           LnGemm384Params lp{};
           lp.X = X; lp.M = orow; lp.ln_g = W(m.nw); lp.ln_b = W(m.nb);
           lp.w = dwh + m.redw; lp.wlo = dwl ? dwl + m.redw : nullptr; lp.b = nullptr;
+          lp.wpk = mergepack;
           lp.out = X2; lp.N = 2 * C; lp.merge_H = g.H; lp.merge_W = g.W;
           timed(mrg_n[s], 2.0 * orow * 4 * C * 2 * C, 4.0 * (double)B * g.H * g.W * C + 8.0 * orow * C +
                 (dwl ? 4.0 : 2.0) * 8.0 * C * C, [&] { launch_lngemm384(lp, stream); });

@@ -123,13 +123,14 @@ struct MlpParams {
   const float* b1;          // [4C]
   const void *w2, *w2lo;    // [C, 4C]
   const float* b2;          // [C]
-  const void* wpack;        // C = 96, 192: W1 | W2 as the kernel's LDS chunk images (launch_mlp_pack)
+  const void* wpack;        // W1 | W2 as the kernel's LDS chunk images (launch_mlp_pack)
 };
 bool mlp_fused_supported(int C);
 void launch_mlp_fused(const MlpParams& p, hipStream_t s);
-// The stage-1/2 MLP kernel's weight chunks in its LDS image order (swizzled, GEMM 2's
-// permuted k order), packed once at load from w1 / w2 (/ lo) so that each 1-KB piece is one
-// contiguous 16-B-per-lane load: mlp_pack_bytes(C, x3) bytes at `out`.
+// The fused MLP kernels' weight chunks in their LDS image order (swizzled, permuted k or
+// unit order), packed once at load from w1 / w2 (/ lo) so that each 1-KB piece -- a staged
+// load at C = 96, 192, an LDS-DMA at C = 384 -- reads 1 KB of contiguous memory:
+// mlp_pack_bytes(C, x3) bytes at `out`.
 size_t mlp_pack_bytes(int C, bool x3);
 void launch_mlp_pack(const MlpParams& p, void* out, hipStream_t s);
 
@@ -145,11 +146,15 @@ struct LnGemm384Params {
   const void *w, *wlo;       // [N, 384] bf16 hi / lo planes
   const float* b;            // [N] or null (no bias)
   float* out;                // [M, N]
+  const void* wpk;           // W as the kernel's LDS chunk images (launch_lngemm384_pack)
   int N;
   int merge_H, merge_W;      // > 0: X is a [B, H, W, 96] map and row r is PatchMerging's
                              // 2 x 2 gather of output pixel r (M = B ceil(H/2) ceil(W/2))
 };
 void launch_lngemm384(const LnGemm384Params& p, hipStream_t s);
+// W [N, 384] (bf16 hi (/ lo) planes) as lngemm384_kernel's LDS chunk images: N * 384 * 2 *
+// (lo ? 2 : 1) bytes at `out`
+void launch_lngemm384_pack(const void* w, const void* wlo, int N, void* out, hipStream_t s);
 
 // Fused norm1 + window qkv + W-MSA + proj + residual of one Swin block (wattn.hip),
 // bf16 / bf16x3 (lo planes present) for C = 96, 192 (head dim 32).

@@ -418,6 +418,42 @@ __device__ __forceinline__ void dma16(const char* gbase, uint32_t voff, uint32_t
       : "memory");
 }
 
+// LDS chunk images of the C = 384 kernels, packed once at load: piece `rem` (1 KB) of plane
+// q of chunk jc at (jc * PL + q) * 24 KB + rem * 1024 + 16 * lane holds the 16 B that lane
+// `lane`'s DMA of that piece gathered from the row-major planes, so the kernels' DMA reads
+// 1 KB of contiguous memory per piece instead of 16 rows x 64 B.
+//  - W1 image (lngemm384's W, mlp384's W1; [N, 384], 32-unit chunks): piece rem = 2 ks + h,
+//    row jc*32 + 4 h + 8 g + (lane / 4) % 4, bytes ks*64 + 16 ((lane & 3) ^ f(lane / 4));
+//  - W2 image (mlp384's W2 [384, 1536]): piece pp, row 16 pp + lane / 4, bytes jc*64 +
+//    16 ((lane & 3) ^ f(lane / 4)).
+__global__ void pack_img384_kernel(const char* __restrict__ hi, const char* __restrict__ lo, int nch, int w2,
+                                   char* __restrict__ out) {
+  constexpr int C = 384, HID = 4 * C, PLB = 32 * C * 2;
+  const int lane = threadIdx.x & 63;
+  const int rem = (int)(blockIdx.x % 24) ;
+  const int q = (int)(blockIdx.x / 24) % (lo ? 2 : 1);
+  const int jc = (int)(blockIdx.x / 24) / (lo ? 2 : 1);
+  if (jc >= nch || threadIdx.x >= 64) return;
+  const int g = lane >> 4;
+  const int chunk16 = ((lane & 3) ^ swz4(lane >> 2)) << 4;
+  size_t src;
+  if (!w2) {
+    const int ks = rem >> 1, h = rem & 1;
+    src = (size_t)(jc * 32 + 4 * h + 8 * g + ((lane >> 2) & 3)) * (C * 2) + ks * 64 + chunk16;
+  } else {
+    src = (size_t)(rem * 16 + (lane >> 2)) * (HID * 2) + jc * 64 + chunk16;
+  }
+  const char* plane = q ? lo : hi;
+  *reinterpret_cast<uint4*>(out + ((size_t)jc * (lo ? 2 : 1) + q) * PLB + rem * 1024 + 16 * lane) =
+      *reinterpret_cast<const uint4*>(plane + src);
+}
+
+void pack_img384(const void* hi, const void* lo, int nch, bool w2, void* out, hipStream_t s) {
+  pack_img384_kernel<<<nch * (lo ? 2 : 1) * 24, 64, 0, s>>>(static_cast<const char*>(hi), static_cast<const char*>(lo),
+                                                            nch, w2 ? 1 : 0, static_cast<char*>(out));
+  MOCR_HIP_CHECK(hipGetLastError());
+}
+
 // timing probes (tools/build_variant.sh DIR -DMOCR_MLP384_PROBE=N; wrong results):
 // 1 no weight DMA, 2 no MFMA, 3 no vmcnt wait before the barriers, 4 every chunk's DMA
 // reads chunk 0 (an L2-resident 96 KB), 5 = 4 + 2
@@ -445,16 +481,16 @@ __global__ void __launch_bounds__(256) mlp384_kernel(MlpParams p) {
   const int j16 = lane & 15;
   const int g = lane >> 4;
   const long row0 = (long)blockIdx.x * 128 + wave * 16 * TT;
-  const char* w1g[2] = {static_cast<const char*>(p.w1), static_cast<const char*>(X3 ? p.w1lo : p.w1)};
-  const char* w2g[2] = {static_cast<const char*>(p.w2), static_cast<const char*>(X3 ? p.w2lo : p.w2)};
+  // the packed chunk images (pack_img384): W1's chunks, then W2's
+  const char* w1g = static_cast<const char*>(p.wpack);
+  const char* w2g = w1g + (size_t)NCH * SLOT;
 
   // W1 piece (plane q, k-step ks, half h): LDS rows u = 16 h + lane / 4 of block ks, slot
   // lane % 4; row u is hidden unit pi(u) = 8 g + 4 h + (lane / 4) % 4 of the chunk, and
   // slot s holds the channel chunk s ^ f(g) of k-step ks.
   // W2 piece (plane q, pp): LDS rows r = 16 pp + lane / 4 (channels), slot s holds the
   // chunk's hidden units 8 (s ^ f(g)) .. + 7.
-  const uint32_t lb1 = (uint32_t)((8 * g + ((lane >> 2) & 3)) * (C * 2) + (((lane & 3) ^ swz4(lane >> 2)) << 4));
-  const uint32_t lb2 = (uint32_t)((lane >> 2) * (HID * 2) + (((lane & 3) ^ swz4(lane >> 2)) << 4));
+  const uint32_t lb1 = (uint32_t)(16 * lane), lb2 = lb1;
   // (the empty asm makes the lane base look new in every call: hipcc would otherwise hoist
   // the 24 per-piece 64-bit addresses out of the chunk loop and spill them)
   // pieces [i0, i0 + n) of this wave's share (the chunk loop issues one piece per MFMA step:
@@ -468,10 +504,9 @@ __global__ void __launch_bounds__(256) mlp384_kernel(MlpParams p) {
       // piece i of this wave: plane q = i / (NPW / PL) (compile-time), piece 4 (i % ..) + wave
       const int q = i / (NPW / PL);
       const int rem = (i - q * (NPW / PL)) * 4 + wave;
-      const int ks = rem >> 1, h = rem & 1;
       const int jr = MOCR_MLP384_PROBE >= 4 ? 0 : jc;
-      const uint32_t off = (uint32_t)((jr * NC + 4 * h) * (C * 2) + ks * 64) + lb;
-      dma16(w1g[q], off, lds_u32(w1s) + q * PLB + rem * 1024);
+      const uint32_t off = (uint32_t)(jr * SLOT + q * PLB + rem * 1024) + lb;
+      dma16(w1g, off, lds_u32(w1s) + q * PLB + rem * 1024);
     }
   };
   auto issue_w2 = [&](int jc, char* w2s, int i0, int n) {
@@ -483,8 +518,8 @@ __global__ void __launch_bounds__(256) mlp384_kernel(MlpParams p) {
       const int q = i / (NPW / PL);
       const int pp = (i - q * (NPW / PL)) * 4 + wave;
       const int jr = MOCR_MLP384_PROBE >= 4 ? 0 : jc;
-      const uint32_t off = (uint32_t)(pp * 16 * (HID * 2) + jr * NC * 2) + lb;
-      dma16(w2g[q], off, lds_u32(w2s) + q * PLB + pp * 1024);
+      const uint32_t off = (uint32_t)(jr * SLOT + q * PLB + pp * 1024) + lb;
+      dma16(w2g, off, lds_u32(w2s) + q * PLB + pp * 1024);
     }
   };
 
@@ -715,11 +750,11 @@ __global__ void __launch_bounds__(256) lngemm384_kernel(LnGemm384Params p) {
   const int N = p.N;
   const int nch = N / NC;
   const long row0 = (long)blockIdx.x * 64 * TT + wave * 16 * TT;
-  const char* wg[2] = {static_cast<const char*>(p.w), static_cast<const char*>(X3 ? p.wlo : p.w)};
+  const char* wpk = static_cast<const char*>(p.wpk);  // the packed chunk images (pack_img384)
 
   // piece i of this wave (plane q = i / (NPW / PL)): LDS rows u = 16 h + lane / 4 of k-step
   // ks's block, unit pi(u) = 8 g + 4 h + (lane / 4) % 4, slot s holds channel chunk s ^ f(g)
-  const uint32_t lb1 = (uint32_t)((8 * g + ((lane >> 2) & 3)) * (C * 2) + (((lane & 3) ^ swz4(lane >> 2)) << 4));
+  const uint32_t lb1 = (uint32_t)(16 * lane);
   auto issue = [&](int jc, char* ws, int i0, int n) {
     uint32_t lb = lb1;
     asm volatile("" : "+v"(lb));
@@ -727,9 +762,8 @@ __global__ void __launch_bounds__(256) lngemm384_kernel(LnGemm384Params p) {
     for (int i = i0; i < i0 + n; ++i) {
       const int q = i / (NPW / PL);
       const int rem = (i - q * (NPW / PL)) * 4 + wave;
-      const int ks = rem >> 1, h = rem & 1;
-      const uint32_t off = (uint32_t)((jc * NC + 4 * h) * (C * 2) + ks * 64) + lb;
-      dma16(wg[q], off, lds_u32(ws) + q * PLB + rem * 1024);
+      const uint32_t off = (uint32_t)(jc * SLOT + q * PLB + rem * 1024) + lb;
+      dma16(wpk, off, lds_u32(ws) + q * PLB + rem * 1024);
     }
   };
   auto slot = [&](int jc) { return ring + (jc % 3) * SLOT; };
@@ -935,7 +969,7 @@ bool mlp_fused_supported(int C) { return C == 96 || C == 192 || C == 384; }
 
 void launch_lngemm384(const LnGemm384Params& p, hipStream_t s) {
   if (p.M <= 0) return;
-  if (p.N <= 0 || p.N % 32 != 0 || p.N > kLnGemm384MaxN || !p.X || !p.w || !p.out || !p.ln_g || !p.ln_b)
+  if (p.N <= 0 || p.N % 32 != 0 || p.N > kLnGemm384MaxN || !p.X || !p.w || !p.wpk || !p.out || !p.ln_g || !p.ln_b)
     throw std::runtime_error("lngemm384: N must be a multiple of 32 up to kLnGemm384MaxN, with every operand");
   if (p.merge_H && (p.merge_H < 1 || p.merge_W < 1 ||
                     p.M % ((long)((p.merge_H + 1) / 2) * ((p.merge_W + 1) / 2)) != 0))
@@ -954,10 +988,15 @@ void launch_lngemm384(const LnGemm384Params& p, hipStream_t s) {
   MOCR_HIP_CHECK(hipGetLastError());
 }
 
-// hidden chunk NC per C as launch_mlp_fused runs the kernel
+// hidden chunk NC per C as launch_mlp_fused runs the kernel; C = 384: W1's then W2's images
 size_t mlp_pack_bytes(int C, bool x3) {
-  if (C != 96 && C != 192) return 0;
-  return (size_t)(x3 ? 2 : 1) * 4 * C * C * 2 * 2;  // NCH chunks x BUF = PL x (W1 + W2) bf16
+  if (C != 96 && C != 192 && C != 384) return 0;
+  return (size_t)(x3 ? 2 : 1) * 4 * C * C * 2 * 2;  // PL x (W1 + W2) bf16
+}
+
+void launch_lngemm384_pack(const void* w, const void* wlo, int N, void* out, hipStream_t s) {
+  if (!w || !out || N <= 0 || N % 32 != 0 || N > kLnGemm384MaxN) throw std::runtime_error("lngemm384_pack: N % 32");
+  pack_img384(w, wlo, N / 32, false, out, s);
 }
 
 void launch_mlp_pack(const MlpParams& p, void* out, hipStream_t s) {
@@ -966,7 +1005,13 @@ void launch_mlp_pack(const MlpParams& p, void* out, hipStream_t s) {
   switch (p.C) {
     case 96: launch_pack_c<96, 64>(p, out, s); break;
     case 192: launch_pack_c<192, 32>(p, out, s); break;
-    default: throw std::runtime_error("mlp_pack: built for C = 96, 192");
+    case 384: {
+      const size_t img = (size_t)4 * 384 * 384 * 2 * (p.w1lo ? 2 : 1);  // W1's 48 chunk images
+      pack_img384(p.w1, p.w1lo, 48, false, out, s);
+      pack_img384(p.w2, p.w2lo, 48, true, static_cast<char*>(out) + img, s);
+      break;
+    }
+    default: throw std::runtime_error("mlp_pack: built for C = 96, 192, 384");
   }
   MOCR_HIP_CHECK(hipGetLastError());
 }
@@ -974,7 +1019,7 @@ void launch_mlp_pack(const MlpParams& p, void* out, hipStream_t s) {
 void launch_mlp_fused(const MlpParams& p, hipStream_t s) {
   if (p.M <= 0) return;
   if ((p.w1lo == nullptr) != (p.w2lo == nullptr)) throw std::runtime_error("mlp: lo planes for both or neither");
-  if ((p.C == 96 || p.C == 192) && !p.wpack) throw std::runtime_error("mlp: packed chunk images (launch_mlp_pack) missing");
+  if (!p.wpack) throw std::runtime_error("mlp: packed chunk images (launch_mlp_pack) missing");
   switch (p.C) {
     // rows per wave 16 TT and hidden chunk NC measured best (TT = 1 at C = 96: 514 vs 420 us
     // per s1 block; TT = 2 at C = 192 spills)
