@@ -1178,12 +1178,13 @@ struct mocr_engine {
   // stage 3 always (285 vs 301 us per block unfused at B=64, 384²); stage 4 only on request
   // (258 vs 211 us: a window's 64 padded rows re-read all of W_qkv, 1.8 GB from L2 per block,
   // and the padding costs 1.3x the GEMM's MFMA work)
-  // stage 3 (C = 384) fused below 128 images: at B = 64 285 vs 301 us per block unfused,
-  // at B = 256 1054 vs 903 us (ln1 + qkv GEMM + window attention over the image tokens,
-  // tools/op_times.py --batch 256, profiles/r03/op_times_b256.log): the fused kernel
-  // re-streams W_qkv per window, the GEMM's efficiency grows with M
-#ifndef MOCR_S3_FUSED_ATTN_LARGE  // A/B builds: the fused stage-3 attention at every batch
-#define MOCR_S3_FUSED_ATTN_LARGE 0
+  // stage 3 (C = 384) fused at every batch since its W_qkv fragments are fragment-major
+  // (round 4): 8.30 vs 8.93 ms per 512-image encode for lngemm384 + the window attention,
+  // bench +1 %, and no fp32 QKV round trip through HBM (profiles/r04/r04x).  Round 3 kept it
+  // below 128 images (1054 vs 903 us per block at B = 256 with row-major fragments,
+  // profiles/r03/op_times_b256.log).  0: lngemm384 + window attention at >= 128 images.
+#ifndef MOCR_S3_FUSED_ATTN_LARGE
+#define MOCR_S3_FUSED_ATTN_LARGE 1
 #endif
   bool noproj_fused(int C, int B) const {
     return attn_fused() && swin_attn_noproj_supported(C) &&
