@@ -1001,12 +1001,10 @@ struct mocr_engine {
       launch_lngemm384_pack(dwh + m.redw, dwl ? dwl + m.redw : nullptr, 192, mergepack, stream);
     }
     int nb = 0;
-    for (int st = 0; st < kStages; ++st)
-      if (stage[st].C <= 384) nb += kDepth[st];
+    for (int st = 0; st < kStages; ++st) nb += kDepth[st];
     if (swinfrag.empty()) swinfrag.resize(nb);
     for (int st = 0, bi = 0; st < kStages; ++st) {
-      const int C = stage[st].C;
-      if (C > 384) break;  // stages 1-3: the fused kernels' W_qkv (+ W_proj at C = 96, 192)
+      const int C = stage[st].C;  // the fused kernels' W_qkv (+ W_proj at C = 96, 192)
       for (int j = 0; j < kDepth[st]; ++j, ++bi) {
         const SwinBlockW& w = lay->blocks[bi];
         for (int m = 0; m < (swin_attn_fused_supported(C) ? 2 : 1); ++m) {
@@ -1322,10 +1320,8 @@ struct mocr_engine {
           ap.ln_b = W(w.n1b);
           ap.wqkv = dwh + w.qkvw;
           ap.wqkv_lo = dwl ? dwl + w.qkvw : nullptr;
-          if (C == 384) {
-            ap.wqkv_fm = swinfrag.at(bi)[0].hi;
-            ap.wqkv_fm_lo = dwl ? swinfrag[bi][0].lo : nullptr;
-          }
+          ap.wqkv_fm = swinfrag.at(bi)[0].hi;
+          ap.wqkv_fm_lo = dwl ? swinfrag[bi][0].lo : nullptr;
           ap.bqkv = W(w.qkvb);
           ap.table = relmask[bi];
           ap.att_hi = ATTh;

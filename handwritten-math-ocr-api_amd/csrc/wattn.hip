@@ -57,15 +57,6 @@ __device__ __forceinline__ floatx4 mma(const bf16x8 (&a)[2], const bf16x8 (&b)[2
   return c;
 }
 
-// 8 bf16 of row `row` (channels ch .. ch+7) of a [rows, C] plane pair
-template <bool X3>
-__device__ __forceinline__ void wfrag(const uint16_t* hi, const uint16_t* lo, int C, int row, int ch,
-                                      bf16x8 (&f)[2]) {
-  const size_t o = (size_t)row * C + ch;
-  f[0] = *reinterpret_cast<const bf16x8*>(hi + o);
-  if constexpr (X3) f[1] = *reinterpret_cast<const bf16x8*>(lo + o);
-}
-
 // timing probes of swin_attn_kernel (tools/build_variant.sh DIR -DMOCR_WATTN_PROBE=N; wrong
 // results): 1 no X loads (LN of zeros), 2 no qkv MFMAs, 3 no attention (S, softmax, PV),
 // 4 no proj MFMAs, 5 no weight loads (qkv and proj fragments from registers), 6 weight
@@ -809,8 +800,15 @@ swin_attn_noproj_ks_kernel(SwinAttnParams p) {
   }
 
   const int h = hg * HPG + wave;  // this wave's head
-  const uint16_t* wqh = static_cast<const uint16_t*>(p.wqkv);
-  const uint16_t* wql = static_cast<const uint16_t*>(p.wqkv_lo);
+  // W_qkv fragment-major (launch_frag_pack), as swin_attn_kernel: fragment (16-row tile,
+  // k-step of all C) = 64 lanes x 16 B
+  const bf16x8* wqh = static_cast<const bf16x8*>(p.wqkv_fm);
+  const bf16x8* wql = static_cast<const bf16x8*>(p.wqkv_fm_lo);
+  auto wfm = [&](int row0, int f, int kstep, bf16x8(&w)[2]) {
+    const int o = (((row0 >> 4) + f) * HEADS + kstep) * 64 + lane;
+    w[0] = wqh[o];
+    if constexpr (X3) w[1] = wql[o];
+  };
   const float* bq = p.bqkv;
   auto xfrag = [&](int ks, int t, bf16x8(&f)[2]) {
     const int r = 16 * t + j16;
@@ -824,7 +822,7 @@ swin_attn_noproj_ks_kernel(SwinAttnParams p) {
     for (int ks = 0; ks < KS; ++ks) {
       bf16x8 w[2][2];
 #pragma unroll
-      for (int f = 0; f < 2; ++f) wfrag<X3>(wqh, wql, C, row0 + 16 * f + j16, k0 + 32 * ks + 8 * g, w[f]);
+      for (int f = 0; f < 2; ++f) wfm(row0, f, k0 / 32 + ks, w[f]);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         bf16x8 xf[2];
@@ -885,7 +883,7 @@ swin_attn_noproj_ks_kernel(SwinAttnParams p) {
     for (int ks = 0; ks < KS; ++ks) {
       bf16x8 w[2][2];
 #pragma unroll
-      for (int f = 0; f < 2; ++f) wfrag<X3>(wqh, wql, C, 2 * C + 32 * h + 16 * f + j16, k0 + 32 * ks + 8 * g, w[f]);
+      for (int f = 0; f < 2; ++f) wfm(2 * C + 32 * h, f, k0 / 32 + ks, w[f]);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         bf16x8 xf[2];
@@ -990,6 +988,8 @@ void launch_swin_attn_noproj(const SwinAttnParams& p, hipStream_t s) {
     throw std::runtime_error("swin_attn_noproj: ATT planes must match the weight planes");
   if (p.heads * 32 != p.C) throw std::runtime_error("swin_attn: head dim must be 32");
   if (p.C != 384 && p.C != 768) throw std::runtime_error("swin_attn_noproj: built for C = 384, 768");
+  if (!p.wqkv_fm || (p.wqkv_lo && !p.wqkv_fm_lo))
+    throw std::runtime_error("swin_attn_noproj: fragment-major W_qkv (launch_frag_pack) missing");
   const unsigned grid = (unsigned)((long)p.B * p.wg.nWin);
   if (p.C == 768) {
     // two workgroups per window, 12 heads (waves) each
@@ -1000,8 +1000,6 @@ void launch_swin_attn_noproj(const SwinAttnParams& p, hipStream_t s) {
     MOCR_HIP_CHECK(hipGetLastError());
     return;
   }
-  if (!p.wqkv_fm || (p.wqkv_lo && !p.wqkv_fm_lo))
-    throw std::runtime_error("swin_attn_noproj: fragment-major W_qkv (launch_frag_pack) missing");
   // 12 waves (one head each, 3 per SIMD, 166 VGPRs) and k-steps unrolled by 2: 285 us per
   // s3 block at B=64, 384² vs 313 (8 waves over the 12 heads, 2 per SIMD), 302 (8 waves,
   // unroll 4), 318 (8 waves, no unroll)
