@@ -81,6 +81,13 @@ __device__ __forceinline__ floatx4 ld_stream_i16x4(const int16_t* base, size_t e
                  (float)((int32_t)w[1] >> 16)};
 }
 
+__device__ __forceinline__ void st_i16x4(int16_t* base, size_t e, const floatx4& v) {  // v: integers
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 w = {((uint32_t)(int)v[0] & 0xffffu) | ((uint32_t)(int)v[1] << 16),
+                   ((uint32_t)(int)v[2] & 0xffffu) | ((uint32_t)(int)v[3] << 16)};
+  *reinterpret_cast<u32x2*>(base + e) = w;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -293,7 +293,9 @@ __device__ unsigned long long g_attn_ts[8192 * 8];
 // the work of a separate argmax kernel at the end of step t-1, without its launch.
 // KVF: K/V (and the self-attention cache) in fp32 (0) or fp24 planes (1, common.h); 2:
 // cross-attention K/V in int16 with per-column scales (the scales of K fold into q, those
-// of V into the output).
+// of V into the output); 3: the self-attention cache in int16 with one scale per (row,
+// head, key) over its 32 values (the key's scale multiplies its score, the value's its
+// softmax weight), the newest key / value quantised here by the same rule.
 // NW waves (8 key rows each per pass; the selection runs on all 64 NW threads).
 template <bool SELF, bool ZS, bool SEL, int NIT, int KVF, int NW>
 __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
@@ -301,8 +303,9 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   MOCR_ATS(1, __builtin_amdgcn_s_memtime());
   constexpr int LPR = 8;  // lanes per key row
   constexpr int RPW = 8;  // key rows per wave instruction
-  constexpr bool F24 = KVF == 1, I16 = KVF == 2;
-  static_assert(!(SELF && I16), "int16 K/V: cross-attention only");
+  constexpr bool F24 = KVF == 1, I16 = KVF == 2, S16 = KVF == 3;
+  static_assert(!(SELF && I16), "int16 K/V with per-column scales: cross-attention only");
+  static_assert(!S16 || SELF, "int16 K/V with per-key scales: the self-attention cache");
   __shared__ floatx4 po[NW][LPR];
   __shared__ float pm[NW], ps[NW];
 
@@ -321,7 +324,9 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
 
   const size_t kvb = KVF ? (size_t)b * p.f24_b + (size_t)h * p.f24_h + li * 4 : (size_t)b * p.kv_b_stride + cc;
   const size_t kvr = KVF ? 32 : (size_t)p.kv_row_stride;
+  const size_t sbase = ((size_t)b * p.f24_b + (size_t)h * p.f24_h) / 32;  // S16: this (row, head)'s key scales
   floatx4 kk[NIT], vv[NIT];
+  float ksc[S16 ? NIT : 1], vsc[S16 ? NIT : 1];
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int m = m_first + it * NW * RPW;
@@ -332,6 +337,12 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
     } else if constexpr (I16) {
       kk[it] = ld_stream_i16x4(p.K16, o);
       vv[it] = ld_stream_i16x4(p.V16, o);
+    } else if constexpr (S16) {
+      kk[it] = ld_stream_i16x4(p.kc16, o);
+      vv[it] = ld_stream_i16x4(p.vc16, o);
+      const size_t so = sbase + (m < n_cached ? m : 0);
+      ksc[it] = p.ksc[so];
+      vsc[it] = p.vsc[so];
     } else {
       kk[it] = ld_stream4(p.K + o);
       vv[it] = ld_stream4(p.V + o);
@@ -393,12 +404,38 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
       zv[2][e] = fp24_round(zv[2][e]);
     }
   }
+  float nks = 1.f, nvs = 1.f;  // S16: the newest key's / value's scale
+  if constexpr (SELF && S16) {
+    // int16 over the head's 32 values (the 8 lanes of a key row hold 4 each): scale max|x| /
+    // 32767; a NaN anywhere makes the scale NaN (fmaxf drops it: tracked apart), so it
+    // reaches the logits and the engine's non-finite check as on the fp32 / fp24 paths
+    auto quant = [&](floatx4& v, float& sc) {
+      float mx = 0.f, nan = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        mx = fmaxf(mx, fabsf(v[e]));
+        nan = v[e] != v[e] ? 1.f : nan;
+      }
+      mx = row_max8(mx);
+      nan = row_max8(nan);
+      const float inv = mx > 0.f ? 32767.f / mx : 0.f;
+      sc = nan != 0.f ? __builtin_nanf("") : (mx > 0.f ? mx / 32767.f : 1.f);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fminf(fmaxf(rintf(v[e] * inv), -32767.f), 32767.f);
+    };
+    quant(zv[1], nks);
+    quant(zv[2], nvs);
+  }
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int m = m_first + it * NW * RPW;
     if constexpr (SELF) {
       kk[it] = m == t ? zv[1] : kk[it];
       vv[it] = m == t ? zv[2] : (m < t ? vv[it] : zero);
+      if constexpr (S16) {
+        ksc[it] = m == t ? nks : ksc[it];
+        vsc[it] = m == t ? nvs : vsc[it];
+      }
     } else {
       vv[it] = m < n ? vv[it] : zero;
     }
@@ -409,6 +446,14 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
         const size_t o = kvb + (size_t)t * 32;
         st_fp24x4(p.kc24, o, zv[1]);
         st_fp24x4(p.vc24, o, zv[2]);
+      } else if constexpr (S16) {
+        const size_t o = kvb + (size_t)t * 32;
+        st_i16x4(p.kc16, o, zv[1]);
+        st_i16x4(p.vc16, o, zv[2]);
+        if (li == 0) {
+          p.ksc[sbase + t] = nks;
+          p.vsc[sbase + t] = nvs;
+        }
       } else {
         const size_t o = kvb + (size_t)t * p.kv_row_stride;
         *reinterpret_cast<floatx4*>(p.kcache + o) = zv[1];
@@ -426,6 +471,7 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
     s = fmaf(q4[2], kk[it][2], s);
     s = fmaf(q4[3], kk[it][3], s);
     s = row_sum<8>(s);  // the 8 lanes of the key row (DPP, as the xor butterfly)
+    if constexpr (S16) s *= ksc[it];
     s *= kAttnScale;
     sc[it] = (m_first + it * NW * RPW < n) ? s : -INFINITY;
     mx = fmaxf(mx, sc[it]);
@@ -438,10 +484,11 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
     for (int it = 0; it < NIT; ++it) {
       const float e = __expf(sc[it] - mx);  // v_exp_f32 (the libm expf's range reduction is ~10 VALU)
       sum += e;
-      o4[0] = fmaf(e, vv[it][0], o4[0]);
-      o4[1] = fmaf(e, vv[it][1], o4[1]);
-      o4[2] = fmaf(e, vv[it][2], o4[2]);
-      o4[3] = fmaf(e, vv[it][3], o4[3]);
+      const float ev = S16 ? e * vsc[it] : e;
+      o4[0] = fmaf(ev, vv[it][0], o4[0]);
+      o4[1] = fmaf(ev, vv[it][1], o4[1]);
+      o4[2] = fmaf(ev, vv[it][2], o4[2]);
+      o4[3] = fmaf(ev, vv[it][3], o4[3]);
     }
   }
   sum = xsum8_16_32(sum);
@@ -546,6 +593,9 @@ void launch_dec_foldattn(const FoldAttnParams& p, bool self_attn, hipStream_t s)
     throw std::runtime_error("foldattn: fp24 K/V needs K and V (and the cache)");
   if (i16 && (self_attn || f24 || !p.V16 || !p.Ks || !p.Vs || p.s_b < kD))
     throw std::runtime_error("foldattn: int16 K/V is cross-attention only, with K, V and their scales");
+  const bool s16 = p.kc16 != nullptr;
+  if (s16 && (!self_attn || f24 || i16 || !p.vc16 || !p.ksc || !p.vsc || p.f24_h % 32 != 0))
+    throw std::runtime_error("foldattn: the int16 cache is self-attention only, with K, V and their scales");
   if (p.B <= 0) return;
   // waves per workgroup: 2 unless the keys exceed 2 x 8 x 10 (tools/attn_ts: the 4-wave
   // kernel's per-wave fixed work -- statistics, unfold, the reductions -- made 8 waves per
@@ -576,6 +626,13 @@ void launch_dec_foldattn(const FoldAttnParams& p, bool self_attn, hipStream_t s)
       dec_foldattn_kernel<false, true, false, N, 2, W><<<grid, 64 * W, 0, s>>>(p);        \
     else                                                                                   \
       dec_foldattn_kernel<false, false, false, N, 2, W><<<grid, 64 * W, 0, s>>>(p);       \
+  } else if (s16) {                                                                        \
+    if (zs)                                                                                \
+      dec_foldattn_kernel<true, true, false, N, 3, W><<<grid, 64 * W, 0, s>>>(p);         \
+    else if (p.sel_on)                                                                     \
+      dec_foldattn_kernel<true, false, true, N, 3, W><<<grid, 64 * W, 0, s>>>(p);         \
+    else                                                                                   \
+      dec_foldattn_kernel<true, false, false, N, 3, W><<<grid, 64 * W, 0, s>>>(p);        \
   } else if (f24) {                                                                        \
     MOCR_FA2(N, 1, W)                                                                      \
   } else {                                                                                 \

@@ -237,7 +237,7 @@ void check_config(const mocr_config& c) {
   req((c.variant & ~(MOCR_VARIANT_UNFUSED_ATTN | MOCR_VARIANT_UNFUSED_MLP | MOCR_VARIANT_DEC_UNFOLDED |
                       MOCR_VARIANT_S4_FUSED_ATTN | MOCR_VARIANT_WINDOW_ROWS | MOCR_VARIANT_DEC_NARROW |
                       MOCR_VARIANT_LOGITS_F32 | MOCR_VARIANT_S3_LARGE_BATCH | MOCR_VARIANT_KV_F32 |
-                      MOCR_VARIANT_CROSS_KV_F24 | MOCR_VARIANT_UNFUSED_LN_GEMM)) == 0,
+                      MOCR_VARIANT_CROSS_KV_F24 | MOCR_VARIANT_UNFUSED_LN_GEMM | MOCR_VARIANT_SELF_KV_F24)) == 0,
       "variant: unknown MOCR_VARIANT_* flag");
   req(c.sos_id >= 0 && c.sos_id < c.vocab && c.eos_id >= 0 && c.eos_id < c.vocab, "special ids");
 }
@@ -324,6 +324,9 @@ struct mocr_engine {
   // packed fp24 (common.h) cross-attention K/V and self-attention cache that the folded
   // greedy step streams in bf16x3 engines (kv24()); 3 bytes per element
   uint8_t *MEMKV24 = nullptr, *kc24 = nullptr, *vc24 = nullptr;
+  // the self-attention cache in int16 with per-(row, head, key) scales (self16())
+  int16_t *kc16 = nullptr, *vc16 = nullptr;
+  float *ksc16 = nullptr, *vsc16 = nullptr;
   // int16 cross-attention K/V (kvx16(), replaces the fp24 planes of MEMKV24) and its
   // per-(layer, row, column) scales [L][max_batch][2d]
   int16_t* MEMKV16 = nullptr;
@@ -394,7 +397,8 @@ struct mocr_engine {
                     ds_sa,   ds_ca,   ds_ff,
                     dlogits_hist, kcache, vcache, ids, feed, forced, finished, logp, st, XWh, XWl, ATTh, ATTl,
                     HIDh, HIDl, MEMh, MEMl, dwh, dwl, kvwh, kvwl, bscore, bfin, bseq[0], bseq[1],
-                    bslot[0], bslot[1], fold_buf, qtab, qpos, dzqkv, dpart, MEMKV24, kc24, vc24, MEMKV16, MEMKVS};
+                    bslot[0], bslot[1], fold_buf, qtab, qpos, dzqkv, dpart, MEMKV24, kc24, vc24, MEMKV16, MEMKVS,
+                    kc16, vc16, ksc16, vsc16};
     for (void* p : bufs)
       if (p) (void)hipFree(p);
     for (void* p : frag_allocs)
@@ -786,8 +790,15 @@ struct mocr_engine {
       } else {
         MEMKV24 = dalloc<uint8_t>(3 * nkv);
       }
-      kc24 = dalloc<uint8_t>(3 * nc);
-      vc24 = dalloc<uint8_t>(3 * nc);
+      if (self16()) {
+        kc16 = dalloc<int16_t>(nc);
+        vc16 = dalloc<int16_t>(nc);
+        ksc16 = dalloc<float>(nc / 32);
+        vsc16 = dalloc<float>(nc / 32);
+      } else {
+        kc24 = dalloc<uint8_t>(3 * nc);
+        vc24 = dalloc<uint8_t>(3 * nc);
+      }
     }
     ld_ids = cfg.max_pos + 1;
     if (cfg.max_beam > 0) {
@@ -1138,8 +1149,11 @@ struct mocr_engine {
     return fold_greedy() && cfg.precision == MOCR_PRECISION_BF16X3 && !(cfg.variant & MOCR_VARIANT_KV_F32);
   }
   // ... with the cross-attention K/V in int16 and per-column scales, unless
-  // MOCR_VARIANT_CROSS_KV_F24 (fp24 as the self-attention cache)
+  // MOCR_VARIANT_CROSS_KV_F24 (fp24)
   bool kvx16() const { return kv24() && !(cfg.variant & MOCR_VARIANT_CROSS_KV_F24); }
+  // ... and the self-attention cache in int16 with one scale per (row, head, key) over its
+  // 32 values (decfold.hip KVF 3), unless MOCR_VARIANT_SELF_KV_F24
+  bool self16() const { return kv24() && !(cfg.variant & MOCR_VARIANT_SELF_KV_F24); }
   // the int16 (or fp24) cross-attention K/V of the B encoded images from MEMKV
   void split_memkv24(int B) {
     if (!kv24()) return;
@@ -1601,7 +1615,11 @@ struct mocr_engine {
       a.K = kc; a.V = vc; a.kcache = kc; a.vcache = vc;
       if (kv24()) {  // head-major [rows][8][max_pos][32] per layer
         const size_t o = l * cache_layer;
-        a.K24 = a.kc24 = kc24 + 3 * o; a.V24 = a.vc24 = vc24 + 3 * o;
+        if (self16()) {
+          a.kc16 = kc16 + o; a.vc16 = vc16 + o; a.ksc = ksc16 + o / 32; a.vsc = vsc16 + o / 32;
+        } else {
+          a.K24 = a.kc24 = kc24 + 3 * o; a.V24 = a.vc24 = vc24 + 3 * o;
+        }
         a.f24_b = (size_t)8 * cfg.max_pos * 32; a.f24_h = (size_t)cfg.max_pos * 32;
       }
       a.kv_b_stride = (size_t)cfg.max_pos * d; a.kv_row_stride = d; a.n = t + 1;
@@ -1885,7 +1903,8 @@ struct mocr_engine {
   }
 
   // Algorithmic work of greedy step t over B rows (as built: fp32, or
-  // bf16x3 weight planes (4 B per weight) and fp24 K/V (3 B) under kv24()): every decoder
+  // bf16x3 weight planes (4 B per weight), int16 cross K/V, and the int16 + scales or fp24
+  // self-attention cache under kv24()): every decoder
   // weight and fc_out once, the cross-attention K/V of all layers, the self-attention K/V
   // of positions 0..t read and position t written, the logits written.  FLOP: the per-row
   // projections 2*(6 d^2 + 2 d ff) per layer + 2 V d, attention 4 d (keys) per layer.
@@ -1895,7 +1914,8 @@ struct mocr_engine {
     const double cross = (double)B * M * 2 * d * L;
     const double self_kv = (double)B * (t + 2) * 2 * d * L;
     const double kvb = kv24() ? 3.0 : 4.0, kvx = kvx16() ? 2.0 : kvb;
-    return 4.0 * (weights + (double)B * V) + kvx * cross + kvb * self_kv;
+    const double kvs = self16() ? 2.0 + 4.0 / 32 : kvb;  // int16 + one fp32 scale per 32 values
+    return 4.0 * (weights + (double)B * V) + kvx * cross + kvs * self_kv;
   }
   double decode_step_flops(int B, int t) const {
     const double d = cfg.d_model, ff = cfg.d_ff, L = cfg.n_layers, V = cfg.vocab;

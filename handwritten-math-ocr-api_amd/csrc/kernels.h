@@ -325,6 +325,11 @@ struct FoldAttnParams {
   const int16_t *K16, *V16;
   const float *Ks, *Vs;
   int s_b;
+  // self-attention only: the cache in int16 (kc16 / vc16, the fp24 layout's element order)
+  // with one scale per (row, head, key) over its 32 values: key m of head h of row b is
+  // kc16[b f24_b + h f24_h + 32 m ..] * ksc[(b f24_b + h f24_h) / 32 + m]
+  int16_t *kc16, *vc16;
+  float *ksc, *vsc;
   size_t kv_b_stride;
   int kv_row_stride;
   int n;                   // keys (self: t + 1)

@@ -36,6 +36,12 @@ __device__ __forceinline__ float row_sum(float s) {
   }
   return s;
 }
+// max over aligned groups of 8 lanes (row_sum<8>'s moves)
+__device__ __forceinline__ float row_max8(float s) {
+  s = fmaxf(s, dpp<0xB1>(s));
+  s = fmaxf(s, dpp<0x4E>(s));
+  return fmaxf(s, dpp<0x141>(s));
+}
 // x[lane ^ 16] and x[lane ^ 32] via v_permlane{16,32}_swap (VALU, no LDS queue).  The
 // swap exchanges halves between two registers, so both start as copies of x and their
 // sum / max is symmetric in the pair.  Inline asm: the builtin with one value for both

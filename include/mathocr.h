@@ -90,9 +90,11 @@ enum {
                                      /* int16 cross-attention K/V                                    */
   MOCR_VARIANT_CROSS_KV_F24 = 512,   /* bf16x3 engines: cross-attention K/V in fp24 instead of int16 */
                                      /* with one scale per (row, column) over the memory's keys      */
-  MOCR_VARIANT_UNFUSED_LN_GEMM = 1024 /* norm + Linear pairs at 384 channels (stage 3's norm1 + qkv  */
+  MOCR_VARIANT_UNFUSED_LN_GEMM = 1024, /* norm + Linear pairs at 384 channels (stage 3's norm1 + qkv */
                                      /* at >= 128 images, merge 1) as two kernels instead of         */
                                      /* mlp.hip's lngemm384_kernel                                   */
+  MOCR_VARIANT_SELF_KV_F24 = 2048    /* bf16x3 engines: the self-attention cache in fp24 instead of  */
+                                     /* int16 with one scale per (row, head, key) over its 32 values */
 };
 
 /* Greedy stopping rule (src/inference.py:23-25). */

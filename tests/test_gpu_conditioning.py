@@ -32,8 +32,9 @@ def outlier_engine(pkg, g, variant=(), max_beam=0):
     return eng
 
 
-@pytest.mark.parametrize("variant,max_beam", [((), 0), ((), 2), (("cross_kv_f24",), 0), (("kv_f32",), 0)],
-                         ids=["int16-epilogue", "int16-pass", "fp24", "fp32"])
+@pytest.mark.parametrize("variant,max_beam", [((), 0), ((), 2), (("cross_kv_f24",), 0), (("self_kv_f24",), 0),
+                                              (("kv_f32",), 0)],
+                         ids=["int16-epilogue", "int16-pass", "fp24", "self-fp24", "fp32"])
 def test_outlier_memory_kv_formats(pkg, golden, variant, max_beam):
     g = golden("g384_b8_outlier")
     m = g["meta"]
@@ -63,8 +64,9 @@ def test_outlier_memory_kv_formats(pkg, golden, variant, max_beam):
     eng.close()
 
 
-@pytest.mark.parametrize("variant,max_beam", [((), 0), ((), 2), (("cross_kv_f24",), 0), (("kv_f32",), 0)],
-                         ids=["int16-epilogue", "int16-pass", "fp24", "fp32"])
+@pytest.mark.parametrize("variant,max_beam", [((), 0), ((), 2), (("cross_kv_f24",), 0), (("self_kv_f24",), 0),
+                                              (("kv_f32",), 0)],
+                         ids=["int16-epilogue", "int16-pass", "fp24", "self-fp24", "fp32"])
 def test_nan_memory_is_reported(pkg, variant, max_beam):
     """One NaN in a memory channel's projection weight makes every cross-attention K/V
     column NaN; the decode must fail with the non-finite-logits error."""
@@ -76,6 +78,24 @@ def test_nan_memory_is_reported(pkg, variant, max_beam):
     eng.load_weights(w)
     eng.encode(pkg.synth.make_images(2, 384, 384, seed0=1000))
     assert np.isnan(eng.memory()[:, :, 5]).all()
+    with pytest.raises(pkg.MocrError, match="non-finite"):
+        eng.decode(max_steps=8, stop="none")
+    eng.close()
+
+
+@pytest.mark.parametrize("variant", [(), ("self_kv_f24",)], ids=["self-int16", "self-fp24"])
+def test_nan_self_attention_is_reported(pkg, variant):
+    """A NaN in one key row of layer 0's self-attention projection makes that head's new keys
+    NaN at every step; on the int16 cache (one scale per key over its 32 values) the scale
+    carries the NaN, so the decode fails with the non-finite-logits error as on fp24."""
+    w = pkg.synth.make_weights(1234, "init")
+    k = "decoder.decoder.layers.0.self_attn.in_proj_weight"
+    iw = w[k].copy()
+    iw[256 + 40, 3] = np.nan  # a row of W_k (rows 256..511), head 1
+    w[k] = iw
+    eng = pkg.Engine(img_hw=(384, 384), max_batch=2, precision="bf16x3", variant=variant)
+    eng.load_weights(w)
+    eng.encode(pkg.synth.make_images(2, 384, 384, seed0=1000))
     with pytest.raises(pkg.MocrError, match="non-finite"):
         eng.decode(max_steps=8, stop="none")
     eng.close()

@@ -122,12 +122,14 @@ def test_teacher_forced_logits_384(pkg, g384):
     np.testing.assert_array_equal(res.ids[:, 1:], g["ids"][:, 1:])
 
 
-@pytest.mark.parametrize("variant", [(), ("logits_f32",), ("kv_f32",), ("cross_kv_f24",)])
+@pytest.mark.parametrize("variant", [(), ("logits_f32",), ("kv_f32",), ("cross_kv_f24",), ("self_kv_f24",)])
 @pytest.mark.parametrize("name", ["g384_b2_pert", "g96x320_b4_eos"])
 def test_teacher_forced_logits_bf16x3(pkg, golden, name, variant):
     """The bench precision (bf16x3 encoder GEMMs, attention, fold GEMMs and logits of the
-    decode step, fp24 K/V; MOCR_VARIANT_LOGITS_F32: fp32 logits; MOCR_VARIANT_KV_F32: fp32
-    K/V): teacher-forced logits within the north star's 1e-3, ids token-exact."""
+    decode step, int16 cross K/V with per-column scales, the int16 self-attention cache
+    with per-key scales; MOCR_VARIANT_LOGITS_F32: fp32 logits; MOCR_VARIANT_KV_F32: fp32
+    K/V; CROSS_KV_F24 / SELF_KV_F24: fp24): teacher-forced logits within the north star's
+    1e-3, ids token-exact."""
     g = golden(name)
     m = g["meta"]
     eng, _ = make_engine(pkg, m, precision="bf16x3", variant=variant)
