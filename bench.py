@@ -443,6 +443,7 @@ def main():
         "rccl_ranks": rccl_ranks,
         "steps": steps,
         "warmup": wcalls * G,
+        "warmup_requested": args.warmup,  # rounded up to whole engine calls of G batches
         "ms_per_step": elapsed / steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",

@@ -228,8 +228,20 @@ __global__ void __launch_bounds__(512) mlp_fused_kernel(MlpParams p) {
 #pragma unroll
     for (int tt = 0; tt < TT; ++tt) acc2[ct][tt] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+  // the residual rows of the epilogue, loaded at the start of the last chunk so that their
+  // HBM round trip runs under its GEMMs (lane (g, j): 4 consecutive channels of row j)
+  floatx4 xres[NCT][TT];
   for (int jc = 0; jc < NCH; ++jc) {
     const bool more = jc + 1 < NCH;
+    if (!more) {
+#pragma unroll
+      for (int tt = 0; tt < TT; ++tt) {
+        const long row = min(row0 + tt * 16 + j16, p.M - 1);
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct)
+          xres[ct][tt] = *reinterpret_cast<const floatx4*>(p.X + (size_t)row * C + ct * 16 + 4 * g);
+      }
+    }
     if (more) {
       stg.load([&](int k) { return piece(jc + 1, k); });
     }
@@ -362,7 +374,7 @@ __global__ void __launch_bounds__(512) mlp_fused_kernel(MlpParams p) {
     for (int ct = 0; ct < NCT; ++ct) {
       const int ch = ct * 16 + 4 * g;
       float* xp = p.X + (size_t)row * C + ch;
-      floatx4 x = *reinterpret_cast<const floatx4*>(xp);
+      floatx4 x = xres[ct][tt];
 #pragma unroll
       for (int r = 0; r < 4; ++r) x[r] = x[r] + (acc2[ct][tt][r] + b2s[ch + r]);
       *reinterpret_cast<floatx4*>(xp) = x;
