@@ -125,7 +125,10 @@ struct TileLds {
   static constexpr int KT = YT ? K1 : K1 + kD;
   static constexpr int UV = 2 * KT * 4;
   static constexpr int AW = (BM / 16) * (X3 ? 2 : 1) * 1024;  // per wave: one step's fragments
-  static constexpr int RED = NW * BM * (BN + 1) * 4;
+  // the reduction's row pitch: 32 x 32 tiles on 8 waves read it 4 columns per lane (16-B
+  // aligned rows), the others one column per lane
+  static constexpr int RP = (BM == 32 && BN == 32 && NW == 8) ? BN + 4 : BN + 1;
+  static constexpr int RED = NW * BM * RP * 4;
   static constexpr int BYTES = UV + NW * AW + RED;
 };
 
@@ -158,7 +161,7 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
   constexpr bool UV = S1 || (S2 && !YT);  // y tiles read A1 only; their LN2 residual uses 16-lane stats
   floatx4* uv_s = reinterpret_cast<floatx4*>(smem);                        // [2][KT / 4]
   char* a_s = smem + L::UV + (threadIdx.x >> 6) * L::AW;                   // this wave's fragments
-  float* red = reinterpret_cast<float*>(smem + L::UV + NW * L::AW);       // [NW][BM][BN + 1]
+  float* red = reinterpret_cast<float*>(smem + L::UV + NW * L::AW);       // [NW][BM][L::RP]
   MOCR_TS(0, __builtin_amdgcn_s_memrealtime());
   MOCR_TS(1, __builtin_amdgcn_s_memtime());
   const int tid = threadIdx.x;
@@ -227,10 +230,33 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
   // = tid & 15 of each 16-column block)
   const int erow = (tid & 255) >> 4;
   const int ecol = tid & 15;
+  // 32 x 32 fold tiles (not the logits): the epilogue takes 4 consecutive columns of one row
+  // per thread (row tid / 8, columns 4 (tid % 8) ..): float4 reduction reads and 16-B stores
+  // instead of one column per thread and 4-B stores
+  constexpr bool V4 = !LOGITS && BM == 32 && BN == 32 && NW == 8;
+  constexpr int RP = L::RP;
+  const int vrow = (tid & 255) >> 3;
+  const int vj = tid & 7;
+  const int vcol = vj * 4;
+  floatx4 vres{}, vbias{}, vg{}, vb{}, vst{};
+  if constexpr (V4) {
+    const int col = (YT ? c0 : c0 - p.NY) + vcol;
+    vbias = *reinterpret_cast<const floatx4*>((YT ? p.by : p.bz) + col);
+    if constexpr (YT) {
+      const int srow = min(r0 + vrow, B - 1);
+      vres = *reinterpret_cast<const floatx4*>(p.A2 + (size_t)srow * kD + c0 + vcol);
+      if constexpr (S2) {
+        vg = *reinterpret_cast<const floatx4*>(p.a2_g + col);
+        vb = *reinterpret_cast<const floatx4*>(p.a2_b + col);
+        // slices 2 vj, 2 vj + 1 of the row's LayerNorm statistics (mean, M2)
+        vst = reinterpret_cast<const floatx4*>(p.a2_stats + (size_t)srow * 2 * kSlices)[vj];
+      }
+    }
+  }
   float rres[YT ? MF : 1][YT ? NF : 1], ebias[NF], eg[YT && S2 ? NF : 1], eb[YT && S2 ? NF : 1];
   float2 est[YT && S2 ? MF : 1];
 #pragma unroll
-  for (int nf = 0; nf < NF; ++nf) {
+  for (int nf = 0; nf < (V4 ? 0 : NF); ++nf) {
     const int col = (YT ? c0 : c0 - p.NY) + nf * 16 + ecol;
     ebias[nf] = (YT ? p.by : p.bz)[col];
     if constexpr (YT && S2) {
@@ -238,7 +264,7 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
       eb[nf] = p.a2_b[col];
     }
   }
-  if constexpr (YT) {
+  if constexpr (YT && !V4) {
 #pragma unroll
     for (int mf = 0; mf < MF; ++mf) {
       const int srow = min(r0 + mf * 16 + erow, B - 1);
@@ -367,10 +393,57 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
 #pragma unroll
     for (int nf = 0; nf < NF; ++nf)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) red[(wave * BM + mf * 16 + g * 4 + r) * (BN + 1) + nf * 16 + li] = acc[mf][nf][r];
+      for (int r = 0; r < 4; ++r) red[(wave * BM + mf * 16 + g * 4 + r) * RP + nf * 16 + li] = acc[mf][nf][r];
   __syncthreads();
   MOCR_TS(4, __builtin_amdgcn_s_memtime());
   if (tid >= 256 || dec_skip(p.st, p.t)) return;
+  if constexpr (V4) {
+    const int orow = r0 + vrow;
+    floatx4 val = *reinterpret_cast<const floatx4*>(red + vrow * RP + vcol);
+#pragma unroll
+    for (int w = 1; w < NW; ++w) val += *reinterpret_cast<const floatx4*>(red + (w * BM + vrow) * RP + vcol);
+    if constexpr (YT) {
+      floatx4 res = vres;
+      if constexpr (S2) {
+        // decoder.hip's fixed merge tree over the 16 slices: level 1 in the lane (slices 2 vj,
+        // 2 vj + 1), then lanes vj ^ 1, ^ 2, ^ 4 -- the pairs row_stats_16lanes_v merges
+        float m = vst[0], q = vst[1];
+        merge_eq(m, q, vst[2], vst[3], 16.f);
+        merge_lanes<1>(m, q, (vj & 1) != 0, 32.f);
+        merge_lanes<2>(m, q, (vj & 2) != 0, 64.f);
+        merge_lanes<4>(m, q, (vj & 4) != 0, 128.f);
+        const float rstd = rstd_of(q);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) res[e] = fmaf((res[e] - m) * rstd, vg[e], vb[e]);
+      }
+      floatx4 y;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y[e] = res[e] + (val[e] + vbias[e]);
+      // the 16-column slice's (mean, M2) over its 4 lanes (quad_perm xor 1, xor 2)
+      float sm = (y[0] + y[1]) + (y[2] + y[3]);
+      sm += dpp<0xB1>(sm);
+      sm += dpp<0x4E>(sm);
+      const float m16 = sm * (1.0f / 16);
+      float qq = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) qq = fmaf(y[e] - m16, y[e] - m16, qq);
+      qq += dpp<0xB1>(qq);
+      qq += dpp<0x4E>(qq);
+      if (orow < B) {
+        *reinterpret_cast<floatx4*>(p.y + (size_t)orow * kD + c0 + vcol) = y;
+        if ((vj & 3) == 0) {
+          float* so = p.y_stats + ((size_t)orow * kSlices + (c0 + vcol) / 16) * 2;
+          so[0] = m16;
+          so[1] = qq;
+        }
+      }
+    } else {
+      if (orow < B) *reinterpret_cast<floatx4*>(p.z + (size_t)orow * p.NZ + (c0 - p.NY) + vcol) = val + vbias;
+    }
+    MOCR_TS(5, __builtin_amdgcn_s_memtime());
+    MOCR_TS(6, __builtin_amdgcn_s_memrealtime());
+    return;
+  }
 #pragma unroll
   for (int mf = 0; mf < MF; ++mf) {
     const int orow = r0 + mf * 16 + erow;
@@ -379,9 +452,9 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
 #pragma unroll
     for (int nf = 0; nf < NF; ++nf) {
       const int lr = mf * 16 + erow, lc = nf * 16 + ecol;
-      float val = red[lr * (BN + 1) + lc];
+      float val = red[lr * RP + lc];
 #pragma unroll
-      for (int w = 1; w < NW; ++w) val += red[(w * BM + lr) * (BN + 1) + lc];
+      for (int w = 1; w < NW; ++w) val += red[(w * BM + lr) * RP + lc];
       const int ocol = c0 + nf * 16 + ecol;
       if constexpr (YT) {
         float res = rres[mf][nf];
