@@ -114,6 +114,19 @@ def auto_chain(steps, replicas, g_max=10):
     return 4
 
 
+def warm_replicas(pool, step):
+    """One untimed call on EVERY replica, each engine driven directly (``pool.imap`` gives an
+    item to whichever replica is free, so a short warm-up may never reach one): each
+    engine's first decode of this (rows, steps, stop) captures and instantiates its 16 graph
+    chunks (engine.hip graph_for), which must not land in the timed region.
+    Returns the engines warmed, in order."""
+    warmed = []
+    for e in pool.engines:
+        step(e, 0)
+        warmed.append(e)
+    return warmed
+
+
 def free_port():
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
@@ -244,23 +257,35 @@ def survey_decode_step_bytes(rows, t, L=8, d=256, ff=512, V=5075, M=144):
     return 2.0 * (weights + rows * M * 2 * d * L + rows * (t + 2) * 2 * d * L)
 
 
+# the greedy steps the committed PMC passes of the decode cover (tools/pmc_traffic.py: an
+# encode and 8 greedy steps, t = 0..7): `traffic` is compared with the algorithmic bytes of
+# these same steps, not with the t = 0..127 average
+PMC_DECODE_STEPS = range(8)
+
+
 def roofline_decode(stats, precision, rows, steps):
     """The greedy decode step (41 graph-captured dependent kernels) against HBM: SURVEY
     §8(d)'s algorithmic bytes of a step (bf16 K/V and weights) / the HIP-event step time,
     with the engine's as-built bytes (engine.hip decode_step_bytes: fp32 weights or their
-    bf16x3 planes, fp24 K/V in bf16x3 engines) beside them."""
+    bf16x3 planes, int16 K/V in bf16x3 engines) beside them.  ``traffic`` (PMC, steps 0..7)
+    is set against ``algorithmic_bytes_pmc_steps``, the §8(d) bytes of the same steps."""
     d = stats.get("decode.greedy")
     if not d or not d["launches"]:
         return None
     step_ms = d["total_ms"] / d["launches"]
     built = d["bytes"] / d["launches"]
     survey = sum(survey_decode_step_bytes(rows, t) for t in range(steps)) / steps
+    pmc_basis = sum(survey_decode_step_bytes(rows, t) for t in PMC_DECODE_STEPS) / len(PMC_DECODE_STEPS)
+    traffic = pmc_traffic(precision, "decode.step", rows)
     achieved = survey / (step_ms * 1e-3) / 1e9
     return {"kernel": f"greedy decode step over {rows} rows (8 layers x 5 folded kernels + logits; the selection "
                       f"runs in the next step's first kernel)", "bound": "hbm",
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "traffic": pmc_traffic(precision, "decode.step", rows), "avg_step_ms": step_ms, "rows": rows,
+            "traffic": traffic, "avg_step_ms": step_ms, "rows": rows,
             "algorithmic_bytes_per_step": survey, "bytes_basis": "SURVEY.md §8(d): bf16 weights and K/V",
+            "traffic_steps": f"t = {PMC_DECODE_STEPS.start}..{PMC_DECODE_STEPS.stop - 1} (the PMC passes' steps)",
+            "algorithmic_bytes_pmc_steps": pmc_basis,
+            "traffic_ratio": traffic / pmc_basis if traffic else None,
             "as_built_bytes_per_step": built, "as_built_achieved": built / (step_ms * 1e-3) / 1e9,
             "as_built_frac": built / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "tflops": d["flops"] / d["launches"] / (step_ms * 1e-3) / 1e12}
@@ -343,6 +368,7 @@ def main():
             lat.append(dt)
         return lat
 
+    warm_replicas(pool, step)
     run(wcalls)
     if world > 1:
         dist.barrier()
@@ -353,10 +379,13 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    rank_elapsed = [elapsed]
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        # every rank's time (an 8-GPU run shows any imbalance); the line's time is the max
+        t = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(t, torch.tensor([elapsed], dtype=torch.float64))
+        rank_elapsed = [float(x.item()) for x in t]
+        elapsed = max(rank_elapsed)
 
     iso = None
     if rank == 0 and args.isolated:
@@ -412,6 +441,7 @@ def main():
         for i, e in enumerate(lit_pool.engines):
             e.set_images(torch.from_numpy(pkg.synth.make_images(B, H, W, seed0=1000 + i * B)).to(dev))
         lit_calls = 32
+        warm_replicas(lit_pool, step)
         run(8, lit_pool)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
@@ -442,7 +472,7 @@ def main():
         "n_gpus": world,
         "rccl_ranks": rccl_ranks,
         "steps": steps,
-        "warmup": wcalls * G,
+        "warmup": (wcalls + R) * G,
         "warmup_requested": args.warmup,  # rounded up to whole engine calls of G batches
         "ms_per_step": elapsed / steps * 1e3,
         "higher_is_better": True,
@@ -454,10 +484,14 @@ def main():
                 + (f", positional table of {max_pos} rows" if args.beam else "")
                 + (", encoder positional table torch seed 5" if args.arch == "res18trans" else "")
                 + f"); {S} {'beam-' + str(args.beam) if args.beam else 'greedy'} steps, no early stop",
-        "config": {"workload": f"B{B} {H}x{W} {'Swin-T' if args.arch == 'swin' else 'ResNet18+8L-enc'} + 8L decoder "
-                               f"{'beam' + str(args.beam) if args.beam else 'greedy'}@{S}, per GPU",
-                   "global_batch": world * B,
-                   "per_gpu_batch": B, "image": [H, W], "max_tokens": S, "vocab": pkg.synth.VOCAB,
+        "config": {"workload": f"{G} x {B} = {BG} images per engine call (one encode, one {BG}-row decode chain), "
+                               f"{R} replicas pipelining, {H}x{W} "
+                               f"{'Swin-T' if args.arch == 'swin' else 'ResNet18+8L-enc'} + 8L decoder "
+                               f"{'beam' + str(args.beam) if args.beam else 'greedy'}@{S}, per GPU; BASELINE "
+                               f"config 2 read literally (64 images per call) is config2_literal",
+                   "global_batch": world * BG,
+                   "per_gpu_batch": BG, "batch_unit": B, "images_per_call": BG, "images_in_flight": BG * R,
+                   "image": [H, W], "max_tokens": S, "vocab": pkg.synth.VOCAB,
                    "decoder_layers": pkg.synth.N_LAYERS, "parallelism": f"image-parallel x{world}", "gather": gather,
                    "replicas_per_gpu": R, "batches_per_chain": G, "precision": args.precision},
         "e2e_roofline": {"value": value / world, "unit": "images/sec per GPU", "peak": E2E_ROOFLINE_IMG_S,
@@ -466,6 +500,10 @@ def main():
         # an image's latency under the bench's load is its engine call's: the call's G batches
         # complete together
         "p50_call_latency_loaded_ms": statistics.median(lat) * 1e3,
+        "latency_samples": len(lat),
+        "warmup_calls": {"per_replica_direct": 1, "pooled": wcalls,
+                         "note": "every replica runs one untimed call (graph capture) before the pooled warm-up"},
+        "rank_elapsed_s": {"min": min(rank_elapsed), "max": max(rank_elapsed), "all": rank_elapsed},
         "p50_image_latency_ms": statistics.median(lat) * 1e3,
         "latency_note": (f"p50_image_latency_ms = p50_call_latency_loaded_ms: the loaded latency of an image's "
                          f"engine call ({G} batch(es) of {B} through encode + decode, {R} replicas pipelining; "

@@ -250,7 +250,7 @@ __device__ __forceinline__ void fold_tile(const FoldGemmParams& p, int c0) {
     const float y = rres + (val + p.by[gcol]);
     p.y[(size_t)grow * kD + gcol] = y;
     const float m16 = row_sum<16>(y) * (1.0f / 16);  // the row's 16 lanes (DPP)
-    const float q = row_sum<16>((y - m16) * (y - m16));
+    const float q = row_sum<16>(sq_rn(y - m16));
     if (col == 0) {
       float* so = p.y_stats + ((size_t)grow * kSlices + c0 / 16) * 2;
       so[0] = m16;
@@ -434,7 +434,9 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
       vv[it] = m == t ? zv[2] : (m < t ? vv[it] : zero);
       if constexpr (S16) {
         ksc[it] = m == t ? nks : ksc[it];
-        vsc[it] = m == t ? nvs : vsc[it];
+        // a masked key's value scale is 0 like its value (e = 0 times a stale NaN scale
+        // would be NaN)
+        vsc[it] = m == t ? nvs : (m < t ? vsc[it] : 0.f);
       }
     } else {
       vv[it] = m < n ? vv[it] : zero;

@@ -221,7 +221,7 @@ __global__ void __launch_bounds__(256) rowgemm_kernel(RowGemmParams p) {
     p.out[(size_t)grow * p.ldo + gcol] = y;
     // (mean, M2) of this row's 16-column slice, reduced over the 16 lanes of the row (DPP)
     const float m16 = row_sum<16>(y) * (1.0f / 16);
-    const float q = row_sum<16>((y - m16) * (y - m16));
+    const float q = row_sum<16>(sq_rn(y - m16));
     if (col == 0) {
       float* so = p.out_stats + ((size_t)grow * kSlices + blockIdx.x) * 2;
       so[0] = m16;

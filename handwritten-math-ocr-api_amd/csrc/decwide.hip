@@ -424,9 +424,8 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
       sm += dpp<0xB1>(sm);
       sm += dpp<0x4E>(sm);
       const float m16 = sm * (1.0f / 16);
-      float qq = 0.f;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) qq = fmaf(y[e] - m16, y[e] - m16, qq);
+      // the pairs row_sum<16> adds: (0 + 1) + (2 + 3) in the lane, then lanes ^ 1, ^ 2
+      float qq = (sq_rn(y[0] - m16) + sq_rn(y[1] - m16)) + (sq_rn(y[2] - m16) + sq_rn(y[3] - m16));
       qq += dpp<0xB1>(qq);
       qq += dpp<0x4E>(qq);
       if (orow < B) {
@@ -461,7 +460,7 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
         if constexpr (S2) res = fmaf((res - mean) * rstd, eg[nf], eb[nf]);
         const float y = res + (val + ebias[nf]);
         const float m16 = row_sum<16>(y) * (1.0f / 16);
-        const float qq = row_sum<16>((y - m16) * (y - m16));
+        const float qq = row_sum<16>(sq_rn(y - m16));
         if (orow < B) {
           p.y[(size_t)orow * kD + ocol] = y;
           if (ecol == 0) {

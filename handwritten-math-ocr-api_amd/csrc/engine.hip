@@ -795,6 +795,10 @@ struct mocr_engine {
         vc16 = dalloc<int16_t>(nc);
         ksc16 = dalloc<float>(nc / 32);
         vsc16 = dalloc<float>(nc / 32);
+        // zeroed (engine stream): a scale slot is read before the step that writes it (the
+        // key loop's masked keys); leftover bytes of a freed engine could be NaN
+        MOCR_HIP_CHECK(hipMemsetAsync(ksc16, 0, nc / 32 * sizeof(float), stream));
+        MOCR_HIP_CHECK(hipMemsetAsync(vsc16, 0, nc / 32 * sizeof(float), stream));
       } else {
         kc24 = dalloc<uint8_t>(3 * nc);
         vc24 = dalloc<uint8_t>(3 * nc);
@@ -2138,13 +2142,15 @@ int mocr_set_cu_mask(mocr_engine* eng, const uint32_t* mask, int n_words) {
     if (n_words && eng->stream_priority != 0)
       throw std::runtime_error("mocr_set_cu_mask: the stream has a priority (mocr_set_stream_priority); HIP makes a "
                                "stream with a CU mask or a priority, not both: set the priority to 0 first");
+    // clearing a mask the stream does not have keeps the stream (and its priority)
+    if (!n_words && !eng->stream_cu_masked) return 0;
     MOCR_HIP_CHECK(hipSetDevice(eng->device));
     MOCR_HIP_CHECK(hipStreamSynchronize(eng->stream));
     hipStream_t s = nullptr;
     if (n_words)
       MOCR_HIP_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)n_words, mask));
     else
-      MOCR_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      MOCR_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));  // masked: priority is 0
     MOCR_HIP_CHECK(hipStreamDestroy(eng->stream));
     eng->stream = s;
     eng->stream_cu_masked = n_words != 0;
@@ -2162,6 +2168,8 @@ int mocr_set_stream_priority(mocr_engine* eng, int priority) {
     if (priority != 0 && eng->stream_cu_masked)
       throw std::runtime_error("mocr_set_stream_priority: the stream has a CU mask (mocr_set_cu_mask); HIP makes a "
                                "stream with a CU mask or a priority, not both: clear the mask first");
+    // the normal priority on a masked stream: the masked stream already has it (mask kept)
+    if (priority == 0 && eng->stream_cu_masked) return 0;
     MOCR_HIP_CHECK(hipStreamSynchronize(eng->stream));
     hipStream_t s = nullptr;
     MOCR_HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio));

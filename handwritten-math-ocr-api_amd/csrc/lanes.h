@@ -36,6 +36,13 @@ __device__ __forceinline__ float row_sum(float s) {
   }
   return s;
 }
+// d * d rounded on its own: never contracted into the add that consumes it, so a LayerNorm
+// slice's M2 has the same bits whichever epilogue shape sums it (row_sum<16> over 16 lanes,
+// or 4 values in a lane and then 4 lanes: the same pairs)
+__device__ __forceinline__ float sq_rn(float d) {
+#pragma clang fp contract(off)
+  return d * d;
+}
 // max over aligned groups of 8 lanes (row_sum<8>'s moves)
 __device__ __forceinline__ float row_max8(float s) {
   s = fmaxf(s, dpp<0xB1>(s));

@@ -221,8 +221,23 @@ def make_res18_fixture(name, *, seed, variant, eos_boost, B, H, W, pos_seed, ste
     print(f"{name}: B={B} {H}x{W} steps={ys.shape[1] - 1} min-margin={model_ref.top2_margins(torch.from_numpy(logits)).min():.2e}")
 
 
+def window_steps(windows, n_steps, width=8):
+    """Step indices of the late teacher-forced logit windows: each entry of ``windows`` is
+    a first step, or "end" for the last ``width`` steps the decode ran (before its stop)."""
+    out = []
+    for w in windows or ():
+        s0 = n_steps - width if w == "end" else int(w)
+        assert 0 <= s0 and s0 + width <= n_steps, (w, n_steps)
+        out.extend(range(s0, s0 + width))
+    return np.asarray(out, dtype=np.int32)
+
+
 def make_batch_fixture(name, *, seed, variant, eos_boost, B, H, W, img_seed=1000, img_kind="uniform",
-                       steps, stop, n_logit_steps, stub, n_mem=2, n_logit_rows=None, proj_outliers=None):
+                       steps, stop, n_logit_steps, stub, n_mem=2, n_logit_rows=None, proj_outliers=None,
+                       windows=None, n_win_rows=8):
+    """``windows``: late windows of 8 steps whose full teacher-forced logit rows are kept
+    for the first ``n_win_rows`` rows (``win_steps`` / ``win_logits``; VERDICT r04: the
+    1e-3 logits bar over the whole decode, where the self-attention cache is long)."""
     pkg = _pkg()
     from oracle import model_ref
     w = apply_proj_outliers(apply_eos_boost(pkg.synth.make_weights(seed, variant), eos_boost), proj_outliers)
@@ -244,19 +259,24 @@ def make_batch_fixture(name, *, seed, variant, eos_boost, B, H, W, img_seed=1000
         assert glue["strings"] == strings, f"{name}: detokenised strings differ"
     top2 = np.sort(logits, -1)[..., -2:]
     margins = (top2[..., 1] - top2[..., 0]).astype(np.float32)
+    ws = window_steps(windows, logits.shape[1])
     np.savez_compressed(
         os.path.join(GOLDEN, name + ".npz"),
         meta=json.dumps(dict(seed=seed, variant=variant, eos_boost=eos_boost, B=B, H=H, W=W, img_seed=img_seed,
                              img_kind=img_kind, steps=steps, stop=stop, glue_checked=glue is not None,
-                             strings=strings, proj_outliers=proj_outliers)),
+                             strings=strings, proj_outliers=proj_outliers, windows=windows,
+                             n_win_rows=n_win_rows if windows else 0)),
         ids=ys.numpy().astype(np.int32),
+        win_steps=ws,
+        win_logits=logits[:n_win_rows, ws].astype(np.float32),
         logits=logits[:(n_logit_rows or n_mem), :n_logit_steps].astype(np.float32),
         margins=margins,
         memory=mem[:n_mem].numpy().astype(np.float32),
         stage_sum=np.array([[float(s[i].double().sum()) for s in stages] for i in range(B)]),
         stage_abs=np.array([[float(s[i].double().abs().sum()) for s in stages] for i in range(B)]),
     )
-    print(f"{name}: ids {tuple(ys.shape)} min-margin {margins.min():.2e} glue={'ok' if glue else '-'}")
+    print(f"{name}: ids {tuple(ys.shape)} min-margin {margins.min():.2e} glue={'ok' if glue else '-'} "
+          f"windows={ws.tolist()}")
 
 
 def make_beam_fixture(name, *, seed, variant, B, H, W, K, steps, max_pos, img_seed=1000, img_kind="uniform"):
@@ -315,23 +335,35 @@ def main(only=None):
         # scaled 30-100x, for the int16 cross-attention K/V (one scale per column over 144 keys)
         make_batch_fixture("g384_b8_outlier", seed=1234, variant="init", eos_boost=0.0, B=8, H=384, W=384,
                            steps=128, stop="batch", n_logit_steps=8, n_logit_rows=8, n_mem=8, stub=stub,
-                           proj_outliers=OUTLIER_ROWS)
+                           proj_outliers=OUTLIER_ROWS, windows=LATE_WINDOWS)
         return
     if only == "bench_c2":
         # config 2 only, teacher-forced logits of 8 rows x 8 steps (VERDICT r02 "Next" 4)
         make_batch_fixture("g384_b64_bench", seed=1234, variant="init", eos_boost=0.0, B=64, H=384, W=384,
-                           steps=128, stop="batch", n_logit_steps=8, n_logit_rows=8, stub=stub)
+                           steps=128, stop="batch", n_logit_steps=8, n_logit_rows=8, stub=stub, windows=LATE_WINDOWS)
+        return
+    if only == "bench_tail":
+        # rows 576-639 of the driver's 640-row chain (images 1576..1639): oracle evidence for
+        # the far end of the as-benched chain (VERDICT r04 "What's weak" 1)
+        make_batch_fixture("g384_b64_tail", seed=1234, variant="init", eos_boost=0.0, B=64, H=384, W=384,
+                           img_seed=1576, steps=128, stop="batch", n_logit_steps=8, n_logit_rows=8, stub=stub,
+                           windows=[120])
         return
     if only == "bench":
         # BASELINE configs at full size, on the bench's own inputs (bench.py: weights seed 1234 "init",
         # images PCG64 1000+i, 384x384): config 2 (Swin, B=64, greedy 128 steps), config 5
         # (ResNet18-trans, B=64, pos table seed 5), config 4 (beam 4, 256 steps: rows 0-1).
         make_batch_fixture("g384_b64_bench", seed=1234, variant="init", eos_boost=0.0, B=64, H=384, W=384,
-                           steps=128, stop="batch", n_logit_steps=8, n_logit_rows=8, stub=stub)
+                           steps=128, stop="batch", n_logit_steps=8, n_logit_rows=8, stub=stub, windows=LATE_WINDOWS)
         make_res18_fixture("r384_b64_bench", seed=1234, variant="init", eos_boost=0.0, B=64, H=384, W=384,
                            pos_seed=5, steps=128, stub=stub, n_logit_steps=4, n_logit_rows=2)
         make_beam_fixture("b384_k4_bench", seed=1234, variant="init", B=2, H=384, W=384, K=4, steps=256,
                           max_pos=260)
+        return
+    if only == "eos":
+        make_batch_fixture("g96x320_b4_eos", seed=21, variant="perturbed", eos_boost=1.72, B=4, H=96, W=320,
+                           img_kind="ink", steps=150, stop="batch", n_logit_steps=4, stub=stub, n_mem=4,
+                           windows=[40, "end"], n_win_rows=4)
         return
     # 384x384, perturbed weights, 128 fixed steps (BASELINE config shape; ids checked via glue with EOS unreachable).
     make_batch_fixture("g384_b2_pert", seed=11, variant="perturbed", eos_boost=0.0, B=2, H=384, W=384,
@@ -342,7 +374,8 @@ def main(only=None):
     # 96x320 serving shape: padded maps, shift disabled on one axis in stages 3-4; EOS reachable so the
     # batch-global stop and post-EOS generation are exercised.
     make_batch_fixture("g96x320_b4_eos", seed=21, variant="perturbed", eos_boost=1.72, B=4, H=96, W=320,
-                       img_kind="ink", steps=150, stop="batch", n_logit_steps=4, stub=stub, n_mem=4)
+                       img_kind="ink", steps=150, stop="batch", n_logit_steps=4, stub=stub, n_mem=4,
+                       windows=[40, "end"], n_win_rows=4)
     # serving im2latex.predict (batch 1, confidence, tokens_to_latex + clean_latex_output)
     make_serving_fixture("serve96x320_eos", seed=21, variant="perturbed", eos_boost=1.72, H=96, W=320,
                          img_seed=1001, img_kind="ink", stub=stub)
@@ -351,6 +384,7 @@ def main(only=None):
 
 
 EOS_BOOST_R18 = 1.6
+LATE_WINDOWS = [56, 120]  # steps 56-63 and 120-127 of the 128-step decodes
 OUTLIER_ROWS = [[3, 30.0], [77, 60.0], [141, 100.0], [200, -80.0]]
 
 if __name__ == "__main__":

@@ -132,3 +132,46 @@ def test_gpus_without_launcher_starts_torchrun_child(bench, monkeypatch):
     assert bench.launch_if_needed(a, [], env={"WORLD_SIZE": "2"}) is None
     with pytest.raises(SystemExit):
         bench.launch_if_needed(a, [], env={"WORLD_SIZE": "4"})
+
+
+def test_warmup_reaches_every_replica(bench, monkeypatch):
+    """The driver's form (--steps 20 --warmup 5: 10-batch calls, 2 replicas, one pooled
+    warm-up call) still warms BOTH replicas before the timed region: each engine's first
+    decode captures its graphs."""
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--steps", "20", "--warmup", "5"])
+    a = bench.parse()
+    assert -(-a.warmup // a.chain) == 1 < a.replicas  # the pooled warm-up alone is one call
+
+    class Pool:
+        engines = [object() for _ in range(a.replicas)]
+
+    seen = []
+    warmed = bench.warm_replicas(Pool, lambda e, k: seen.append(e))
+    assert seen == Pool.engines and warmed == Pool.engines
+
+
+def test_decode_traffic_on_the_steps_it_was_measured(bench, monkeypatch):
+    """`traffic` of the decode step comes from PMC passes over steps 0..7: its ratio is taken
+    against the SURVEY §8(d) bytes of those steps, not the t = 0..127 average."""
+    monkeypatch.setattr(bench, "pmc_traffic", lambda precision, cls, rows: 1.256e9)
+    st = {"decode.greedy": rec(128, 0.52, 1e9, 9e8)}
+    r = bench.roofline_decode(st, "bf16x3", 640, 128)
+    early = sum(bench.survey_decode_step_bytes(640, t) for t in range(8)) / 8
+    assert r["algorithmic_bytes_pmc_steps"] == pytest.approx(early)
+    assert r["traffic_ratio"] == pytest.approx(1.256e9 / early)
+    assert r["algorithmic_bytes_per_step"] > early  # the t = 0..127 average (longer caches)
+
+
+def test_gpus8_without_launcher_starts_eight_ranks(bench, monkeypatch):
+    """The driver's N = 8 form without a launcher: one torch.distributed.run child with 8
+    local ranks on 127.0.0.1."""
+    seen = {}
+
+    class Done:
+        returncode = 0
+
+    monkeypatch.setattr(bench.subprocess, "run", lambda cmd, *a, **k: seen.setdefault("cmd", cmd) and Done())
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "20", "--warmup", "5"])
+    a = bench.parse()
+    assert bench.launch_if_needed(a, ["--gpus", "8", "--steps", "20", "--warmup", "5"], env={}) == 0
+    assert "--nproc-per-node=8" in seen["cmd"] and "--master-addr=127.0.0.1" in seen["cmd"]

@@ -16,6 +16,7 @@ import json
 import numpy as np
 import pytest
 
+from conftest import check_logit_windows
 from oracle.gen_golden import apply_proj_outliers
 
 pytestmark = pytest.mark.gpu
@@ -61,6 +62,7 @@ def test_outlier_memory_kv_formats(pkg, golden, variant, max_beam):
                                        "rows_equal": int(sum(np.array_equal(res.ids[i], g["ids"][i])
                                                              for i in range(g["ids"].shape[0])))}))
     assert err < LOGIT_TOL, err
+    check_logit_windows(tf.logits, g, label=f"g384_b8_outlier {'+'.join(variant) or 'int16'} beam{max_beam}")
     eng.close()
 
 
@@ -99,3 +101,31 @@ def test_nan_self_attention_is_reported(pkg, variant):
     with pytest.raises(pkg.MocrError, match="non-finite"):
         eng.decode(max_steps=8, stop="none")
     eng.close()
+
+
+def test_engine_after_nan_poisoned_engine(pkg):
+    """The int16 self-attention cache's value scales of keys not yet written are read by the
+    key loop (masked by a zero weight): they are zeroed at allocation and masked in the
+    kernel, so an engine allocated where a NaN-poisoned engine's cache was freed decodes as a
+    fresh one."""
+    w = pkg.synth.make_weights(1234, "init")
+    imgs = pkg.synth.make_images(2, 384, 384, seed0=1000)
+
+    def run(weights):
+        eng = pkg.Engine(img_hw=(384, 384), max_batch=2, precision="bf16x3")
+        eng.load_weights(weights)
+        eng.encode(imgs)
+        try:
+            return eng.decode(max_steps=24, stop="none").ids
+        finally:
+            eng.close()
+
+    clean = run(w)
+    bad = dict(w)
+    k = "decoder.decoder.layers.0.self_attn.in_proj_weight"
+    iw = w[k].copy()
+    iw[512:768, :] = np.nan  # W_v: every value (and value scale) of the cache is NaN
+    bad[k] = iw
+    with pytest.raises(pkg.MocrError, match="non-finite"):
+        run(bad)
+    np.testing.assert_array_equal(run(w), clean)

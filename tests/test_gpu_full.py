@@ -21,6 +21,8 @@ import json
 import numpy as np
 import pytest
 
+from conftest import check_logit_windows
+
 pytestmark = pytest.mark.gpu
 
 LOGIT_TOL = 1e-3
@@ -52,7 +54,10 @@ def check_ids(got, ref, margins, tie, record=None):
     return n_full
 
 
-def check_teacher_forced(eng, ref_ids, margins, tie, ref_logits):
+def check_teacher_forced(eng, ref_ids, margins, tie, ref_logits, g=None, label=""):
+    """Teacher-forced decode on the fixture's ids: argmax of every step above the tie
+    margin, the first steps' logits and (``g`` with late windows) the logits at steps
+    56-63 / 120-127, where the self-attention cache holds 57-128 keys, within 1e-3."""
     S = ref_ids.shape[1] - 1
     tf = eng.decode(max_steps=S, stop="none", forced=ref_ids, want_logits=True)
     am = tf.logits.argmax(-1)
@@ -62,6 +67,8 @@ def check_teacher_forced(eng, ref_ids, margins, tie, ref_logits):
     r, n = ref_logits.shape[:2]
     err = float(np.abs(tf.logits[:r, :n] - ref_logits).max())
     assert err < LOGIT_TOL, err
+    if g is not None and "win_steps" in g:
+        check_logit_windows(tf.logits, g, label=label)
 
 
 # rows of the 64 that equal the fixture over all 129 columns, near-tie rows included
@@ -69,23 +76,25 @@ def check_teacher_forced(eng, ref_ids, margins, tie, ref_logits):
 C2_ROWS_EQUAL_FLOOR = {"bf16x3": 64, "fp32": 64}
 
 
-@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
-def test_config2_swin_b64_greedy128(pkg, golden, precision):
+@pytest.mark.parametrize("precision,variant", [("bf16x3", ()), ("fp32", ()), ("bf16x3", ("self_kv_f24",))],
+                         ids=["bf16x3", "fp32", "bf16x3-self_kv_f24"])
+def test_config2_swin_b64_greedy128(pkg, golden, precision, variant):
     g = golden("g384_b64_bench")
     m = g["meta"]
     assert (m["B"], m["H"], m["W"], m["steps"], m["seed"], m["variant"]) == (64, 384, 384, 128, 1234, "init")
-    eng = pkg.Engine(img_hw=(384, 384), max_batch=64, precision=precision)
+    eng = pkg.Engine(img_hw=(384, 384), max_batch=64, precision=precision, variant=variant)
     eng.load_weights(pkg.synth.make_weights(1234, "init"))
     eng.encode(pkg.synth.make_images(64, 384, 384, seed0=1000))
     mem = eng.memory()
     assert rel_err(mem[:2], g["memory"]) < 1e-4
     res = eng.decode(max_steps=128, stop="batch")
     assert res.n_steps == g["ids"].shape[1] - 1
-    rec = {"config": "C2", "precision": precision}
+    rec = {"config": "C2", "precision": precision, "variant": list(variant)}
     n_full = check_ids(res.ids, g["ids"], g["margins"], tie=1e-4, record=rec)
     assert n_full >= 60, n_full
     assert rec["rows_equal_all_columns"] >= C2_ROWS_EQUAL_FLOOR[precision], rec
-    check_teacher_forced(eng, g["ids"], g["margins"], 1e-4, g["logits"])
+    check_teacher_forced(eng, g["ids"], g["margins"], 1e-4, g["logits"], g,
+                         label=f"C2 B=64 {precision} {'+'.join(variant) or 'production'}")
     # determinism at full size, and the bench's no-stop decode gives the same tokens
     again = eng.decode(max_steps=128, stop="none")
     np.testing.assert_array_equal(again.ids, res.ids)
@@ -126,19 +135,45 @@ def test_config2_as_benched_b256_chain(pkg, golden):
 def test_config2_as_benched_640_chain(pkg, golden):
     """Config 2 the way the driver's `bench.py --steps 20` runs it: ten 64-image batches
     encoded as one 640-image batch and decoded as one 640-row chain (above 256 rows the
-    FFN fold GEMM keeps two k steps in flight, decwide.hip launch_fw_nw; the MFMA sequence
-    per output is the same).  Rows 0-63 are the fixture's images."""
+    FFN fold GEMM keeps two k steps in flight, decwide.hip launch_fw_nw; above 480 rows every
+    fold GEMM takes the vectorised 32 x 32 epilogue).  Rows 0-63 are the g384_b64_bench
+    fixture's images and rows 576-639 the g384_b64_tail fixture's (images 1576-1639), both
+    pinned by the reference's own glue: ids, and teacher-forced logits of the first and the
+    late windows (steps 56-63, 120-127) within 1e-3 on the production int16 caches."""
     g = golden("g384_b64_bench")
+    gt = golden("g384_b64_tail")
+    assert gt["meta"]["img_seed"] == 1576
     imgs = pkg.synth.make_images(640, 384, 384, seed0=1000)
     eng = pkg.Engine(img_hw=(384, 384), max_batch=640, precision="bf16x3")
     eng.load_weights(pkg.synth.make_weights(1234, "init"))
     eng.encode(imgs)
-    assert rel_err(eng.memory()[:2], g["memory"]) < 1e-4
+    mem = eng.memory()
+    assert rel_err(mem[:2], g["memory"]) < 1e-4
+    assert rel_err(mem[576:578], gt["memory"]) < 1e-4
+    del mem
     res = eng.decode(max_steps=128, stop="none")
     rec = {"config": "C2 as benched by the driver (B=640 encode, 640-row chain)", "precision": "bf16x3"}
     n_full = check_ids(res.ids[:64], g["ids"], g["margins"], tie=1e-4, record=rec)
     assert n_full >= 60, n_full
     assert rec["rows_equal_all_columns"] >= C2_ROWS_EQUAL_FLOOR["bf16x3"], rec
+    rec = {"config": "C2 as benched, rows 576-639 (g384_b64_tail)", "precision": "bf16x3"}
+    n_full = check_ids(res.ids[576:], gt["ids"], gt["margins"], tie=1e-4, record=rec)
+    assert n_full >= 53, n_full  # 11 of the fixture's 64 rows hold a step with a margin below 1e-4
+    assert rec["rows_equal_all_columns"] >= 64, rec  # measured on MI355X: all 64, tie rows included
+    # teacher forcing over the whole chain: the fixtures' ids on their rows, the engine's own
+    # greedy ids on the others
+    forced = res.ids.copy()
+    forced[:64] = g["ids"]
+    forced[576:] = gt["ids"]
+    tf = eng.decode(max_steps=128, stop="none", forced=forced, want_logits=True)
+    for fx, r0, name in ((g, 0, "rows 0-63"), (gt, 576, "rows 576-639")):
+        r, n = fx["logits"].shape[:2]
+        err = float(np.abs(tf.logits[r0:r0 + r, :n] - fx["logits"]).max())
+        assert err < LOGIT_TOL, (name, err)
+        ok = fx["margins"] >= 1e-4
+        np.testing.assert_array_equal(tf.logits[r0:r0 + 64].argmax(-1)[ok], fx["ids"][:, 1:][ok])
+        check_logit_windows(tf.logits, fx, row0=r0, label=f"C2 640-row chain {name}")
+    del tf
     # the last 64 rows decode as they do in a 64-row chain of their own (rows are
     # independent: same memory bits, same per-row k order at any chain length)
     e64 = pkg.Engine(img_hw=(384, 384), max_batch=64, precision="bf16x3", variant=("s3_large_batch",))

@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 import torch
 
+from conftest import check_logit_windows
 from oracle import model_ref
 from oracle.gen_golden import apply_eos_boost
 
@@ -141,6 +142,8 @@ def test_teacher_forced_logits_bf16x3(pkg, golden, name, variant):
     err = float(np.abs(res.logits[:, :n] - g["logits"]).max())
     print(f"{name} bf16x3 teacher-forced logits max|d| = {err:.2e}")
     assert err < LOGIT_TOL, err
+    if "win_steps" in g:  # the late windows, up to the last steps before the global stop
+        check_logit_windows(res.logits, g, label=f"{name} bf16x3 {'+'.join(variant) or 'production'}")
     margins = g["margins"]
     ok = margins >= 1e-4  # near-ties a different fp32 summation order may flip
     assert np.array_equal(res.ids[:, 1:][ok], g["ids"][:, 1:][ok])
@@ -232,6 +235,30 @@ def test_batch_invariance_384(pkg, g384):
     res = eng.decode(max_steps=g["meta"]["steps"], stop="none")
     np.testing.assert_array_equal(res.ids[0], g["ids"][1])
     eng.close()
+
+
+def test_long_chain_rows_bitwise(pkg, g384):
+    """A 520-row chain (above 480 rows every fold GEMM takes decwide.hip's 32 x 32 tiles
+    with the vectorised epilogue, and the FFN keeps two k steps in flight) gives rows 0-1
+    bitwise the logits of the 2-row chain (16-row tiles, one column per thread): the
+    LayerNorm slice statistics sum the same pairs with the same rounding in both epilogue
+    shapes.  Both encodes run stage 3 on its large-batch kernels, so the
+    memory is bitwise equal too."""
+    g, _, w, imgs = g384
+    S = 24
+    big = np.concatenate([imgs, pkg.synth.make_images(518, 384, 384, seed0=5000)], 0)
+    out, mem = {}, {}
+    for rows, x in ((520, big), (2, imgs)):
+        eng = pkg.Engine(img_hw=(384, 384), max_batch=rows, precision="bf16x3", variant=("s3_large_batch",))
+        eng.load_weights(w)
+        eng.encode(x)
+        mem[rows] = eng.memory()[:2]
+        r = eng.decode(max_steps=S, stop="none", want_logits=True)
+        out[rows] = (r.ids[:2].copy(), r.logits[:2].copy())
+        eng.close()
+    np.testing.assert_array_equal(mem[520], mem[2])
+    np.testing.assert_array_equal(out[520][0], out[2][0])
+    np.testing.assert_array_equal(out[520][1], out[2][1])
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
@@ -347,8 +374,16 @@ def test_cu_mask_and_priority_exclude_each_other(pkg):
     eng.set_cu_mask(range(128))
     with pytest.raises(pkg.MocrError, match="CU mask"):
         eng.set_stream_priority(1)
+    # the normal priority on a masked stream keeps the mask: still refused
+    eng.set_stream_priority(0)
+    with pytest.raises(pkg.MocrError, match="CU mask"):
+        eng.set_stream_priority(1)
     eng.set_cu_mask(None)
     eng.set_stream_priority(1)
+    with pytest.raises(pkg.MocrError, match="priority"):
+        eng.set_cu_mask(range(64))
+    # clearing a mask the stream does not have keeps its priority: a mask is still refused
+    eng.set_cu_mask(None)
     with pytest.raises(pkg.MocrError, match="priority"):
         eng.set_cu_mask(range(64))
     eng.set_stream_priority(0)

@@ -38,8 +38,12 @@ def test_oracle_reproduces_golden_96x320_batch_stop(pkg, golden):
     imgs = torch.from_numpy(pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m["img_kind"]))
     mem = model_ref.encode(model, imgs)
     np.testing.assert_allclose(mem.numpy(), g["memory"], atol=1e-5)
-    ys, _ = model_ref.greedy_decode(model, memory=mem, max_steps=m["steps"], stop="batch")
+    ys, logits = model_ref.greedy_decode(model, memory=mem, max_steps=m["steps"], stop="batch", record_logits=True)
     np.testing.assert_array_equal(ys.numpy(), g["ids"])
+    # the late teacher-forced windows (steps 40-47 and the last 8 before the global stop)
+    logits = torch.stack(logits, 1).numpy()
+    assert g["win_steps"].tolist() == list(range(40, 48)) + list(range(ys.shape[1] - 9, ys.shape[1] - 1))
+    np.testing.assert_allclose(logits[:, g["win_steps"]], g["win_logits"], atol=1e-5)
 
 
 def test_detokenize_matches_reference_strings(pkg, golden):
