@@ -83,6 +83,8 @@ def parse():
                     help="res18trans: BASELINE config 5 (src/model_res18trans.py)")
     ap.add_argument("--beam", type=int, default=0,
                     help="K > 0: beam search (BASELINE config 4: --beam 4 --batch 32 --tokens 256)")
+    ap.add_argument("--variant", default="",
+                    help="comma-separated engine.VARIANT names (A/B of a kernel path; empty = production)")
     ap.add_argument("--lib", default=None,
                     help="an in-tree A/B build of libmathocr.so (tools/build_variant.sh) instead of lib/")
     a = ap.parse_args()
@@ -328,8 +330,9 @@ def main():
     # 256 beam-search tokens need a positional table of >= 257 rows (the reference's has 150,
     # src/model_swin.py:54): synthetic weights with 260 rows for that config
     max_pos = max(pkg.synth.MAX_POS, S + 4) if args.beam else pkg.synth.MAX_POS
+    variant = tuple(v for v in args.variant.split(",") if v)
     ekw = dict(img_hw=(H, W), max_batch=BG, precision=args.precision, device=local, arch=args.arch,
-               max_beam=args.beam, max_pos=max_pos)
+               max_beam=args.beam, max_pos=max_pos, variant=variant)
     pool = pkg.pipeline.ReplicaPool(R, **ekw)
     if gather.startswith("rccl"):
         # after the engines: their HIP streams take the process's first hardware queues
@@ -493,7 +496,8 @@ def main():
                    "per_gpu_batch": BG, "batch_unit": B, "images_per_call": BG, "images_in_flight": BG * R,
                    "image": [H, W], "max_tokens": S, "vocab": pkg.synth.VOCAB,
                    "decoder_layers": pkg.synth.N_LAYERS, "parallelism": f"image-parallel x{world}", "gather": gather,
-                   "replicas_per_gpu": R, "batches_per_chain": G, "precision": args.precision},
+                   "replicas_per_gpu": R, "batches_per_chain": G, "precision": args.precision,
+                   "variant": list(variant)},
         "e2e_roofline": {"value": value / world, "unit": "images/sec per GPU", "peak": E2E_ROOFLINE_IMG_S,
                          "frac": value / world / E2E_ROOFLINE_IMG_S,
                          "basis": "BASELINE.md §4: 26.39 GFLOP/img at 2.5 PF + 245 MB/img bf16 decode traffic at 8 TB/s"},

@@ -297,7 +297,7 @@ __device__ unsigned long long g_attn_ts[8192 * 8];
 // head, key) over its 32 values (the key's scale multiplies its score, the value's its
 // softmax weight), the newest key / value quantised here by the same rule.
 // NW waves (8 key rows each per pass; the selection runs on all 64 NW threads).
-template <bool SELF, bool ZS, bool SEL, int NIT, int KVF, int NW>
+template <bool SELF, bool ZS, bool SEL, int NIT, int KVF, int NW, bool SLOT = false>
 __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   MOCR_ATS(0, __builtin_amdgcn_s_memrealtime());
   MOCR_ATS(1, __builtin_amdgcn_s_memtime());
@@ -322,15 +322,33 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   const int n_cached = SELF ? t : n;
   const int m_first = wave * RPW + rsub;
 
-  const size_t kvb = KVF ? (size_t)b * p.f24_b + (size_t)h * p.f24_h + li * 4 : (size_t)b * p.kv_b_stride + cc;
+  static_assert(!SLOT || (SELF && !SEL), "slot tables: the self-attention of beam hypotheses");
+  // the K/V row: this decoder row, its image's memory row (cross-attention of beam
+  // hypotheses: mem_div of them per image), or per key its slot row (SLOT, below)
+  const int mb = SELF ? b : (p.mem_div > 1 ? b / p.mem_div : b);
+  auto row_base = [&](int r) -> size_t {
+    return KVF ? (size_t)r * p.f24_b + (size_t)h * p.f24_h + li * 4 : (size_t)r * p.kv_b_stride + cc;
+  };
+  const size_t kvb = row_base(mb);
   const size_t kvr = KVF ? 32 : (size_t)p.kv_row_stride;
   const size_t sbase = ((size_t)b * p.f24_b + (size_t)h * p.f24_h) / 32;  // S16: this (row, head)'s key scales
+  int srow[SLOT ? NIT : 1];
+  if constexpr (SLOT) {
+    // key m < t of hypothesis b lives in the cache row of the ancestor that computed it; a
+    // stale entry (after a batch stop) is clamped to a valid row
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int m = m_first + it * NW * RPW;
+      const int sr = p.slot_rows[(size_t)b * p.slot_ld + (m < n_cached ? m : 0)];
+      srow[it] = (unsigned)sr < (unsigned)p.B ? sr : 0;
+    }
+  }
   floatx4 kk[NIT], vv[NIT];
   float ksc[S16 ? NIT : 1], vsc[S16 ? NIT : 1];
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int m = m_first + it * NW * RPW;
-    const size_t o = kvb + (size_t)(m < n_cached ? m : 0) * kvr;  // row 0 is allocated; masked below
+    const size_t o = (SLOT ? row_base(srow[it]) : kvb) + (size_t)(m < n_cached ? m : 0) * kvr;  // masked below
     if constexpr (F24) {
       kk[it] = ld_stream_fp24x4(p.K24, o);
       vv[it] = ld_stream_fp24x4(p.V24, o);
@@ -340,7 +358,7 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
     } else if constexpr (S16) {
       kk[it] = ld_stream_i16x4(p.kc16, o);
       vv[it] = ld_stream_i16x4(p.vc16, o);
-      const size_t so = sbase + (m < n_cached ? m : 0);
+      const size_t so = (SLOT ? ((size_t)srow[it] * p.f24_b + (size_t)h * p.f24_h) / 32 : sbase) + (m < n_cached ? m : 0);
       ksc[it] = p.ksc[so];
       vsc[it] = p.vsc[so];
     } else {
@@ -393,8 +411,8 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   floatx4 q4 = zv[0];
   floatx4 vs4;
   if constexpr (I16) {
-    q4 *= *reinterpret_cast<const floatx4*>(p.Ks + (size_t)b * p.s_b + cc);
-    vs4 = *reinterpret_cast<const floatx4*>(p.Vs + (size_t)b * p.s_b + cc);
+    q4 *= *reinterpret_cast<const floatx4*>(p.Ks + (size_t)mb * p.s_b + cc);
+    vs4 = *reinterpret_cast<const floatx4*>(p.Vs + (size_t)mb * p.s_b + cc);
   }
   const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
   if constexpr (SELF && F24) {  // the newest key / value as every later step reads them from the cache
@@ -646,6 +664,39 @@ void launch_dec_foldattn(const FoldAttnParams& p, bool self_attn, hipStream_t s)
     break;
   if ((nw == 2 && nit > 10) || (nw == 1 && nit > 5))
     throw std::runtime_error("foldattn: at most 160 keys on 2 waves, 40 on 1");
+  if (p.slot_rows) {
+    // beam hypotheses' self-attention: the int16 cache (bf16x3 engines) or fp32 (fp32 engines)
+    if (!self_attn || p.sel_on || f24 || p.slot_ld < p.n) throw std::runtime_error("foldattn: slot tables need "
+                                                                                   "self-attention on the int16 or fp32 cache");
+#define MOCR_FS(N, W)                                                                          \
+  case N:                                                                                      \
+    if (s16 && zs) dec_foldattn_kernel<true, true, false, N, 3, W, true><<<grid, 64 * W, 0, s>>>(p);       \
+    else if (s16) dec_foldattn_kernel<true, false, false, N, 3, W, true><<<grid, 64 * W, 0, s>>>(p);       \
+    else if (zs) dec_foldattn_kernel<true, true, false, N, 0, W, true><<<grid, 64 * W, 0, s>>>(p);         \
+    else dec_foldattn_kernel<true, false, false, N, 0, W, true><<<grid, 64 * W, 0, s>>>(p);                \
+    break;
+    if (nw == 4) {
+      switch (nit) {
+        MOCR_FS(1, 4) MOCR_FS(2, 4) MOCR_FS(3, 4) MOCR_FS(4, 4) MOCR_FS(5, 4) MOCR_FS(6, 4) MOCR_FS(7, 4) MOCR_FS(8, 4)
+        MOCR_FS(9, 4)
+        default: throw std::runtime_error("foldattn: at most 288 keys");
+      }
+    } else if (nw == 2) {
+      switch (nit) {
+        MOCR_FS(1, 2) MOCR_FS(2, 2) MOCR_FS(3, 2) MOCR_FS(4, 2) MOCR_FS(5, 2) MOCR_FS(6, 2) MOCR_FS(7, 2) MOCR_FS(8, 2)
+        MOCR_FS(9, 2) MOCR_FS(10, 2)
+        default: break;
+      }
+    } else {
+      switch (nit) {
+        MOCR_FS(1, 1) MOCR_FS(2, 1) MOCR_FS(3, 1) MOCR_FS(4, 1) MOCR_FS(5, 1)
+        default: break;
+      }
+    }
+#undef MOCR_FS
+    MOCR_HIP_CHECK(hipGetLastError());
+    return;
+  }
   if (nw == 4) {
     switch (nit) {
       MOCR_FA(1, 4) MOCR_FA(2, 4) MOCR_FA(3, 4) MOCR_FA(4, 4) MOCR_FA(5, 4) MOCR_FA(6, 4) MOCR_FA(7, 4) MOCR_FA(8, 4)

@@ -581,6 +581,9 @@ __global__ void __launch_bounds__(256) beam_init_kernel(BeamParams p) {
   const int r = blockIdx.x;
   for (int c = threadIdx.x; c < p.d; c += blockDim.x)
     p.x[(size_t)r * p.d + c] = p.emb[(size_t)p.sos * p.d + c] + p.pos[c];
+  if (p.qtab)  // folded step: layer 0's q|k|v of sos at position 0
+    for (int c = threadIdx.x; c < 3 * p.d; c += blockDim.x)
+      p.z[(size_t)r * 3 * p.d + c] = p.qtab[(size_t)p.sos * 3 * p.d + c] + p.qpos[c];
   if (threadIdx.x == 0) {
     p.score[r] = (r % p.K == 0) ? 0.f : -INFINITY;
     p.fin[r] = 0;
@@ -755,6 +758,12 @@ __global__ void __launch_bounds__(256) beam_select_kernel(BeamParams p) {
       const int k = i / p.d, c = i - k * p.d;
       p.x[(size_t)(b * K + k) * p.d + c] = p.emb[(size_t)s_tok[k] * p.d + c] + p.pos[(size_t)(t + 1) * p.d + c];
     }
+    if (p.qtab)
+      for (int i = tid; i < K * 3 * p.d; i += 256) {
+        const int k = i / (3 * p.d), c = i - k * 3 * p.d;
+        p.z[(size_t)(b * K + k) * 3 * p.d + c] =
+            p.qtab[(size_t)s_tok[k] * 3 * p.d + c] + p.qpos[(size_t)(t + 1) * 3 * p.d + c];
+      }
   }
 }
 

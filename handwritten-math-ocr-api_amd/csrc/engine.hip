@@ -237,7 +237,8 @@ void check_config(const mocr_config& c) {
   req((c.variant & ~(MOCR_VARIANT_UNFUSED_ATTN | MOCR_VARIANT_UNFUSED_MLP | MOCR_VARIANT_DEC_UNFOLDED |
                       MOCR_VARIANT_S4_FUSED_ATTN | MOCR_VARIANT_WINDOW_ROWS | MOCR_VARIANT_DEC_NARROW |
                       MOCR_VARIANT_LOGITS_F32 | MOCR_VARIANT_S3_LARGE_BATCH | MOCR_VARIANT_KV_F32 |
-                      MOCR_VARIANT_CROSS_KV_F24 | MOCR_VARIANT_UNFUSED_LN_GEMM | MOCR_VARIANT_SELF_KV_F24)) == 0,
+                      MOCR_VARIANT_CROSS_KV_F24 | MOCR_VARIANT_UNFUSED_LN_GEMM | MOCR_VARIANT_SELF_KV_F24 |
+                      MOCR_VARIANT_BEAM_UNFOLDED)) == 0,
       "variant: unknown MOCR_VARIANT_* flag");
   req(c.sos_id >= 0 && c.sos_id < c.vocab && c.eos_id >= 0 && c.eos_id < c.vocab, "special ids");
 }
@@ -849,7 +850,7 @@ struct mocr_engine {
       }
       qtab = dalloc<float>((size_t)cfg.vocab * 3 * d);
       qpos = dalloc<float>((size_t)cfg.max_pos * 3 * d);
-      dzqkv = dalloc<float>(B * 3 * d);
+      dzqkv = dalloc<float>(R * 3 * d);  // rows: images, or hypotheses (beam search)
     }
     ids = dalloc<int32_t>(B * ld_ids);
     feed = dalloc<int32_t>(B * ld_ids);
@@ -1158,6 +1159,11 @@ struct mocr_engine {
   // ... and the self-attention cache in int16 with one scale per (row, head, key) over its
   // 32 values (decfold.hip KVF 3), unless MOCR_VARIANT_SELF_KV_F24
   bool self16() const { return kv24() && !(cfg.variant & MOCR_VARIANT_SELF_KV_F24); }
+  // beam search on the folded step (int16 or fp32 self-attention cache through slot
+  // tables), unless MOCR_VARIANT_BEAM_UNFOLDED or a cache format the slot kernels lack (fp24)
+  bool beam_folded() const {
+    return fold_greedy() && !(cfg.variant & MOCR_VARIANT_BEAM_UNFOLDED) && (self16() || !kv24());
+  }
   // the int16 (or fp24) cross-attention K/V of the B encoded images from MEMKV
   void split_memkv24(int B) {
     if (!kv24()) return;
@@ -1597,7 +1603,9 @@ struct mocr_engine {
   // self-attention (q|k|v unfolded from dzqkv: layer 0's from the embedding tables, later
   // layers' from the previous FFN kernel), out_proj + z_q, cross-attention (q unfolded),
   // out_proj + z_h, FFN (hidden unfolded from z_h) + the next layer's z_qkv.
-  void record_layers_fold(int B, int t, const DecodeState* stp) {
+  // slots / mem_div: beam search (rows = hypotheses, self-attention keys through the
+  // slot table of step t, memory row = row / mem_div); nullptr / 1 for greedy decoding.
+  void record_layers_fold(int B, int t, const DecodeState* stp, const int32_t* slots = nullptr, int mem_div = 1) {
     const int d = cfg.d_model, L = cfg.n_layers;
     const size_t cache_layer = (size_t)max_rows * cfg.max_pos * d;
     const size_t kv_layer = (size_t)cfg.max_batch * M * 2 * d;
@@ -1627,6 +1635,7 @@ struct mocr_engine {
         a.f24_b = (size_t)8 * cfg.max_pos * 32; a.f24_h = (size_t)cfg.max_pos * 32;
       }
       a.kv_b_stride = (size_t)cfg.max_pos * d; a.kv_row_stride = d; a.n = t + 1;
+      a.slot_rows = slots; a.slot_ld = ld_ids;
       launch_dec_foldattn(a, true, s);
       FoldGemmParams g{};
       g.B = B; g.t = t; g.st = stp;
@@ -1641,6 +1650,7 @@ struct mocr_engine {
       a = FoldAttnParams{};
       a.st = stp; a.t = t; a.B = B; a.out = datt; a.z = dq; a.z_ld = d; a.z_stats = ds_sa; a.s = f.sq; a.c = f.cq;
       a.K = memk; a.V = memk + d; a.kv_b_stride = (size_t)M * 2 * d; a.kv_row_stride = 2 * d; a.n = M;
+      a.mem_div = mem_div;
       if (kv24()) {  // head-major [B][k | v][8][M][32] per layer
         const size_t o = l * kv_layer, ov = o + (size_t)8 * M * 32;
         if (kvx16()) {
@@ -1773,14 +1783,38 @@ struct mocr_engine {
     b.emb = W(lay->emb);
     b.pos = W(lay->pos);
     b.x = dx;
+    if (beam_folded()) {
+      b.qtab = qtab;
+      b.qpos = qpos;
+      b.z = dzqkv;
+    }
     return b;
   }
 
   // One beam-search step over B images x K hypotheses (oracle/model_ref.py beam_search).
+  // Folded (production): the greedy step's kernels over the B*K hypothesis rows, the
+  // self-attention through the slot table, the logits on decwide.hip's tiles into the full
+  // rows beam_select_kernel reads.  MOCR_VARIANT_BEAM_UNFOLDED: round 2's projection +
+  // attention kernels and row GEMMs on fp32 K/V.
   void record_beam_step(int B, int K, int t, int max_steps, bool stop_batch) {
     const DecodeState* stp = stop_batch ? st : nullptr;
-    record_layers(B * K, t, stp, bslot[t & 1], K);
-    record_logits(B * K, t, stp, dlogits, 0);
+    if (beam_folded()) {
+      record_layers_fold(B * K, t, stp, bslot[t & 1], K);
+      if (fold_wide()) {
+        const DecLayerW& last = lay->layers[cfg.n_layers - 1];
+        FoldGemmParams g{};
+        g.B = B * K; g.t = t; g.st = stp; g.K1 = 0; g.NY = 0;
+        g.A2 = dy_ff; g.a2_stats = ds_ff; g.a2_g = W(last.n3w); g.a2_b = W(last.n3b);
+        g.Wz = fcw_pad; g.bz = fcb_pad; g.z = dlogits; g.NZ = Vpad; g.n_valid = cfg.vocab;
+        g.Fz_hi = frag_logits.hi; g.Fz_lo = frag_logits.lo; g.Fz = frag_logits.f;
+        launch_foldwide(g, stream);
+      } else {
+        record_logits(B * K, t, stp, dlogits, 0);
+      }
+    } else {
+      record_layers(B * K, t, stp, bslot[t & 1], K);
+      record_logits(B * K, t, stp, dlogits, 0);
+    }
     launch_beam_select(beam_params(B, K, t, max_steps, stop_batch), stream);
   }
 

@@ -342,6 +342,12 @@ struct FoldAttnParams {
   SelectArgs sel;
   const float *qtab, *qpos, *emb, *pos;
   float* x;
+  // beam search (rows = hypotheses): self-attention key m < t of row b lives in cache row
+  // slot_rows[b * slot_ld + m] (the hypothesis' ancestor that computed it); the
+  // cross-attention reads memory row b / mem_div (0: 1)
+  const int32_t* slot_rows;
+  int slot_ld;
+  int mem_div;
 };
 void launch_dec_foldattn(const FoldAttnParams& p, bool self_attn, hipStream_t s);
 
@@ -406,6 +412,10 @@ struct BeamParams {
   const float* emb;
   const float* pos;
   float* x;                 // [B*K, d] next step's input
+  // folded step (qtab set): layer 0's q|k|v of each new hypothesis' token at position t+1,
+  // z[r] = qtab[tok] + qpos[t + 1] ([B*K, 3d], decfold.hip's table lookup)
+  const float *qtab, *qpos;
+  float* z;
 };
 void launch_beam_init(const BeamParams& p, hipStream_t s);
 void launch_beam_select(const BeamParams& p, hipStream_t s);

@@ -27,7 +27,7 @@ ABI_VERSION = 6
 # kernel-path variants (include/mathocr.h MOCR_VARIANT_*): 0 = production
 VARIANT = {"unfused_attn": 1, "unfused_mlp": 2, "dec_unfolded": 4, "s4_fused_attn": 8, "window_rows": 16, "dec_narrow": 32,
            "logits_f32": 64, "s3_large_batch": 128, "kv_f32": 256,
-           "cross_kv_f24": 512, "unfused_ln_gemm": 1024, "self_kv_f24": 2048}
+           "cross_kv_f24": 512, "unfused_ln_gemm": 1024, "self_kv_f24": 2048, "beam_unfolded": 4096}
 
 
 class MocrConfig(ctypes.Structure):

@@ -93,8 +93,10 @@ enum {
   MOCR_VARIANT_UNFUSED_LN_GEMM = 1024, /* norm + Linear pairs at 384 channels (stage 3's norm1 + qkv */
                                      /* at >= 128 images, merge 1) as two kernels instead of         */
                                      /* mlp.hip's lngemm384_kernel                                   */
-  MOCR_VARIANT_SELF_KV_F24 = 2048    /* bf16x3 engines: the self-attention cache in fp24 instead of  */
+  MOCR_VARIANT_SELF_KV_F24 = 2048,   /* bf16x3 engines: the self-attention cache in fp24 instead of  */
                                      /* int16 with one scale per (row, head, key) over its 32 values */
+  MOCR_VARIANT_BEAM_UNFOLDED = 4096  /* beam search on round 2's projection+attention step (fp32     */
+                                     /* K/V, row GEMMs) instead of the folded wide-tile step         */
 };
 
 /* Greedy stopping rule (src/inference.py:23-25). */

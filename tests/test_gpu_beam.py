@@ -10,6 +10,9 @@ Checks:
   EOS fixtures do);
 * 256 steps with a 260-row positional table (BASELINE config 4's length): beam = 1
   equals greedy up to EOS, and beam = 4 is deterministic with scores in rank order.
+Every check runs on the production beam step (the greedy step's folded kernels over the
+hypothesis rows: self-attention through the slot tables, the int16 caches of bf16x3
+engines) and on MOCR_VARIANT_BEAM_UNFOLDED (round 2's projection + attention kernels).
 """
 import numpy as np
 import pytest
@@ -23,10 +26,10 @@ pytestmark = pytest.mark.gpu
 SCORE_TOL = 1e-3
 
 
-def run_case(pkg, precision, eos_boost, steps, stop, B=2, K=4, H=96, W=320, seed=1234):
+def run_case(pkg, precision, eos_boost, steps, stop, B=2, K=4, H=96, W=320, seed=1234, variant=()):
     w = apply_eos_boost(pkg.synth.make_weights(seed, "perturbed"), eos_boost)
     imgs = pkg.synth.make_images(B, H, W, seed0=1000)
-    eng = pkg.Engine(img_hw=(H, W), max_batch=B, precision=precision, max_beam=K)
+    eng = pkg.Engine(img_hw=(H, W), max_batch=B, precision=precision, max_beam=K, variant=variant)
     eng.load_weights(w)
     eng.encode(imgs)
     res = eng.beam_search(beam=K, max_steps=steps, stop=stop)
@@ -39,9 +42,13 @@ def run_case(pkg, precision, eos_boost, steps, stop, B=2, K=4, H=96, W=320, seed
     return res, seqs.numpy(), scores.numpy(), n
 
 
+VARIANTS = pytest.mark.parametrize("variant", [(), ("beam_unfolded",)], ids=["folded", "unfolded"])
+
+
+@VARIANTS
 @pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
-def test_beam_matches_oracle(pkg, precision):
-    res, seqs, scores, n = run_case(pkg, precision, eos_boost=0.0, steps=16, stop="none")
+def test_beam_matches_oracle(pkg, precision, variant):
+    res, seqs, scores, n = run_case(pkg, precision, eos_boost=0.0, steps=16, stop="none", variant=variant)
     assert res.n_steps == n == 16
     np.testing.assert_array_equal(res.beams, seqs)
     assert np.abs(res.scores - scores).max() <= SCORE_TOL
@@ -50,9 +57,11 @@ def test_beam_matches_oracle(pkg, precision):
     assert np.abs(np.diff(scores, axis=1)).min() > 10 * SCORE_TOL
 
 
-def test_beam_finished_hypotheses_and_stop(pkg):
+@VARIANTS
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+def test_beam_finished_hypotheses_and_stop(pkg, precision, variant):
     # EOS boosted so hypotheses finish at different steps and the batch stops early
-    res, seqs, scores, n = run_case(pkg, "fp32", eos_boost=4.0, steps=40, stop="batch")
+    res, seqs, scores, n = run_case(pkg, precision, eos_boost=4.0, steps=40, stop="batch", variant=variant)
     assert res.n_steps == n < 40
     np.testing.assert_array_equal(res.beams, seqs)
     assert np.abs(res.scores - scores).max() <= SCORE_TOL
@@ -65,11 +74,12 @@ def test_beam_finished_hypotheses_and_stop(pkg):
             assert (row[hits[0] + 1:] == pkg.synth.PAD_ID).all(), "finished hypotheses are padded"
 
 
-def test_beam_long_sequences(pkg):
+@VARIANTS
+def test_beam_long_sequences(pkg, variant):
     max_pos, steps, B = 260, 256, 2
     w = pkg.synth.make_weights(1234, "perturbed", max_pos=max_pos)
     imgs = pkg.synth.make_images(B, 96, 320, seed0=1000)
-    eng = pkg.Engine(img_hw=(96, 320), max_batch=B, precision="fp32", max_pos=max_pos, max_beam=4)
+    eng = pkg.Engine(img_hw=(96, 320), max_batch=B, precision="fp32", max_pos=max_pos, max_beam=4, variant=variant)
     eng.load_weights(w)
     eng.encode(imgs)
     g = eng.decode(max_steps=steps, stop="none")
