@@ -264,6 +264,11 @@ StageGeom make_win(int H, int W, int C, int heads) {
   return g;
 }
 
+// stage 3 (C = 384) on its fused attention kernel at every batch (see noproj_fused)
+#ifndef MOCR_S3_FUSED_ATTN_LARGE
+#define MOCR_S3_FUSED_ATTN_LARGE 1
+#endif
+
 template <typename T>
 T* dalloc(size_t n) {
   void* p = nullptr;
@@ -1023,7 +1028,10 @@ struct mocr_engine {
       const int C = stage[st].C;  // the fused kernels' W_qkv (+ W_proj at C = 96, 192)
       for (int j = 0; j < kDepth[st]; ++j, ++bi) {
         const SwinBlockW& w = lay->blocks[bi];
-        for (int m = 0; m < (swin_attn_fused_supported(C) ? 2 : 1); ++m) {
+        // W_qkv fragments: the fused attention kernels of stages 1-3 (stage 4 only under
+        // MOCR_VARIANT_S4_FUSED_ATTN), W_proj at C = 96, 192
+        const bool qkv_frags = attn_fused() && (C != 768 || (cfg.variant & MOCR_VARIANT_S4_FUSED_ATTN));
+        for (int m = qkv_frags ? 0 : 1; m < (swin_attn_fused_supported(C) ? 2 : (qkv_frags ? 1 : 0)); ++m) {
           FragW& f = swinfrag[bi][m];
           const int N = m == 0 ? 3 * C : C;
           if (!f.hi) {
@@ -1048,7 +1056,10 @@ struct mocr_engine {
           mp.w2lo = dwl ? dwl + w.fc2w : nullptr;
           launch_mlp_pack(mp, mlppack[bi], stream);
         }
-        if (C == 384) {
+        // lngemm384's W_qkv image: stage 3's norm1 + qkv runs on it only when its fused
+        // attention kernel does not (MOCR_VARIANT_UNFUSED_ATTN, or a MOCR_S3_FUSED_ATTN_LARGE=0
+        // build at >= 128 images)
+        if (C == 384 && (!attn_fused() || !MOCR_S3_FUSED_ATTN_LARGE) && !(cfg.variant & MOCR_VARIANT_UNFUSED_LN_GEMM)) {
           if (lngpack.size() <= (size_t)bi) lngpack.resize(bi + 1, nullptr);
           if (!lngpack[bi]) {
             lngpack[bi] = dalloc<char>((size_t)3 * C * C * 2 * (dwl ? 2 : 1));
@@ -1205,9 +1216,6 @@ struct mocr_engine {
   // bench +1 %, and no fp32 QKV round trip through HBM (profiles/r04/r04x).  Round 3 kept it
   // below 128 images (1054 vs 903 us per block at B = 256 with row-major fragments,
   // profiles/r03/op_times_b256.log).  0: lngemm384 + window attention at >= 128 images.
-#ifndef MOCR_S3_FUSED_ATTN_LARGE
-#define MOCR_S3_FUSED_ATTN_LARGE 1
-#endif
   bool noproj_fused(int C, int B) const {
     return attn_fused() && swin_attn_noproj_supported(C) &&
            (C != 768 || (cfg.variant & MOCR_VARIANT_S4_FUSED_ATTN)) &&

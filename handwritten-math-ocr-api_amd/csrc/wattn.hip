@@ -65,8 +65,11 @@ __device__ __forceinline__ floatx4 mma(const bf16x8 (&a)[2], const bf16x8 (&b)[2
 #ifndef MOCR_WATTN_PROBE
 #define MOCR_WATTN_PROBE 0
 #endif
-template <int C, int PASSES, int OCC>
-__global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC))) swin_attn_kernel(SwinAttnParams p) {
+// WPB windows per workgroup, HEADS waves each: the waves of one head in the WPB windows
+// load the same weight fragments at the same point of the same instruction stream (the
+// block's barriers keep them in step), so the CU's L1 can serve the later ones.
+template <int C, int PASSES, int OCC, int WPB>
+__global__ void __launch_bounds__(2 * C * WPB) __attribute__((amdgpu_waves_per_eu(OCC))) swin_attn_kernel(SwinAttnParams p) {
   constexpr bool X3 = PASSES == 3;
   constexpr int PL = X3 ? 2 : 1;
   constexpr int HEADS = C / 32;  // = waves = k-steps of every GEMM here
@@ -78,16 +81,23 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
   constexpr int XB = 64 * C * 2;  // bytes per plane: the LN'd window, later proj's B fragments
   constexpr int LPR = C / 12;     // lanes per row in the LayerNorm (12 floats each)
   static_assert(RC % SW == 0 && 64 % LPR == 0, "layout");
-  __shared__ __attribute__((aligned(16))) char lds[PL * XB];
+  __shared__ __attribute__((aligned(16))) char lds_all[WPB * PL * XB];
 
-  const int tid = threadIdx.x;
+  const int wsub = (int)threadIdx.x / NT;    // this wave's window within the workgroup
+  const int tid = (int)threadIdx.x - wsub * NT;
+  char* const lds = lds_all + wsub * PL * XB;
   const int lane = tid & 63;
   const int h = tid >> 6;
   const int j16 = lane & 15;
   const int g = lane >> 4;
   const WinGeom& wg = p.wg;
-  const int b = (int)(blockIdx.x / (unsigned)wg.nWin);
-  const int win = (int)(blockIdx.x - (unsigned)b * wg.nWin);
+  // a window past the last (odd window count) recomputes the last one and stores nothing
+  const long nwin_all = (long)p.B * wg.nWin;
+  const long gw_raw = (long)blockIdx.x * WPB + wsub;
+  const bool live = gw_raw < nwin_all;
+  const long gw = live ? gw_raw : nwin_all - 1;
+  const int b = (int)(gw / wg.nWin);
+  const int win = (int)(gw - (long)b * wg.nWin);
   const int wy = win / wg.nWx;
   const int wx = win - wy * wg.nWx;
   // X row of window token tk, -1 for the padded tokens and slots 49..63
@@ -411,7 +421,7 @@ __global__ void __launch_bounds__(2 * C) __attribute__((amdgpu_waves_per_eu(OCC)
     const floatx4 bp = *reinterpret_cast<const floatx4*>(p.bproj + ch);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      if (pxo[t] < 0) continue;
+      if (pxo[t] < 0 || !live) continue;
       floatx4 xv = xres[f][t];
 #pragma unroll
       for (int r = 0; r < 4; ++r) xv[r] = xv[r] + (ap[f][t][r] + bp[r]);
@@ -950,14 +960,22 @@ swin_attn_noproj_ks_kernel(SwinAttnParams p) {
                           p.att_hi, p.att_lo);
 }
 
-template <int C, int OCC>
+template <int C, int OCC, int WPB>
 void launch_c(const SwinAttnParams& p, hipStream_t s) {
-  const unsigned grid = (unsigned)((long)p.B * p.wg.nWin);
+  const unsigned grid = (unsigned)(((long)p.B * p.wg.nWin + WPB - 1) / WPB);
   if (p.wqkv_lo)
-    swin_attn_kernel<C, 3, OCC><<<grid, 2 * C, 0, s>>>(p);
+    swin_attn_kernel<C, 3, OCC, WPB><<<grid, 2 * C * WPB, 0, s>>>(p);
   else
-    swin_attn_kernel<C, 1, OCC><<<grid, 2 * C, 0, s>>>(p);
+    swin_attn_kernel<C, 1, OCC, WPB><<<grid, 2 * C * WPB, 0, s>>>(p);
 }
+// windows per workgroup (A/B builds: tools/build_variant.sh DIR -DMOCR_S1_WPB=2); at C = 192
+// two windows need 3 waves per SIMD (12 waves per workgroup)
+#ifndef MOCR_S1_WPB
+#define MOCR_S1_WPB 1
+#endif
+#ifndef MOCR_S2_WPB
+#define MOCR_S2_WPB 1
+#endif
 
 // waves per SIMD the register allocation targets: 3 at C = 96 (534 vs 651 us per s1
 // block, 19 dwords spilled), 2 at C = 192 (509 vs 649 us: 94 spilled at 3).
@@ -975,8 +993,8 @@ void launch_swin_attn_fused(const SwinAttnParams& p, hipStream_t s) {
     throw std::runtime_error("swin_attn: fragment-major weights (launch_frag_pack) missing");
   if (p.heads * 32 != p.C) throw std::runtime_error("swin_attn: head dim must be 32");
   switch (p.C) {
-    case 96: launch_c<96, 3>(p, s); break;
-    case 192: launch_c<192, 2>(p, s); break;
+    case 96: launch_c<96, 3, MOCR_S1_WPB>(p, s); break;
+    case 192: launch_c<192, MOCR_S2_WPB == 1 ? 2 : 3, MOCR_S2_WPB>(p, s); break;
     default: throw std::runtime_error("swin_attn: fused attention built for C = 96, 192");
   }
   MOCR_HIP_CHECK(hipGetLastError());
