@@ -73,14 +73,12 @@ struct StgList<N, N> {
   __device__ __forceinline__ void store(G) const {}
 };
 
-// Piece k (1 KB, 16 B per lane) of a wave's share of one W1 | W2 chunk: plane k / KPL,
-// piece (k % KPL) * 8 + wave of that plane's [W1 image | W2 image]: the 16 bytes of lane
-// `lane` (two 8-B loads, whichever image) and their LDS offset.  Both images' addresses
-// are computed and selected (no divergent branch).
-template <int C, int NC, int PL, int DMA1, int KPL, int RC, int SW1, int SH1, int RB, int SH2>
-__device__ __forceinline__ uint4 mlp_piece_load(const MlpParams& p, int jc, int k, int wave, int lane) {
-  const int q = k / KPL;
-  const int rem = (k - q * KPL) * 8 + wave;
+// Piece rem (1 KB, 16 B per lane) of plane q of one W1 | W2 chunk's LDS image: pieces
+// 0 .. DMA1 - 1 are the W1 image, the rest the W2 image.  The 16 bytes of lane `lane`
+// (two 8-B loads, whichever image) and their offset in the image (the LDS byte order:
+// [W1 planes | W2 planes]).  Both images' addresses are computed and selected.
+template <int C, int NC, int DMA1, int RC, int SW1, int SH1, int RB, int SH2>
+__device__ __forceinline__ uint4 mlp_piece_load(const MlpParams& p, int jc, int q, int rem, int lane) {
   const bool in1 = rem < DMA1;
   const int sl = (in1 ? rem : rem - DMA1) * 64 + lane;
   // W1 image: row r1 = hidden unit, slot = 8 channels, XOR-swizzled
@@ -99,17 +97,15 @@ __device__ __forceinline__ uint4 mlp_piece_load(const MlpParams& p, int jc, int 
   const uint2 hi = *reinterpret_cast<const uint2*>(in1 ? a1 + 8 : a2 + 32);
   return make_uint4(lo.x, lo.y, hi.x, hi.y);
 }
-template <int PL, int DMA1, int KPL, int W1B, int W2B>
-__device__ __forceinline__ int mlp_piece_dst(int k, int wave, int lane) {
-  const int q = k / KPL;
-  const int rem = (k - q * KPL) * 8 + wave;
+template <int PL, int DMA1, int W1B, int W2B>
+__device__ __forceinline__ int mlp_piece_dst(int q, int rem, int lane) {
   const bool in1 = rem < DMA1;
   const int sl = (in1 ? rem : rem - DMA1) * 64 + lane;
   return in1 ? q * W1B + sl * 16 : PL * W1B + q * W2B + sl * 16;
 }
 
-template <int C, int TT, int NC, int PASSES>
-__global__ void __launch_bounds__(512) mlp_fused_kernel(MlpParams p) {
+template <int C, int TT, int NC, int PASSES, int NWV = 8>
+__global__ void __launch_bounds__(64 * NWV) mlp_fused_kernel(MlpParams p) {
   constexpr bool X3 = PASSES == 3;
   constexpr int PL = X3 ? 2 : 1;
   constexpr int RC = C / 8;  // 16-B chunks per W1 row
@@ -129,14 +125,15 @@ __global__ void __launch_bounds__(512) mlp_fused_kernel(MlpParams p) {
   constexpr int KP = NC / 32;
   constexpr int HID = 4 * C;
   constexpr int NCH = HID / NC;
-  constexpr int ROWS = 8 * 16 * TT;
-  constexpr int DMA1 = W1B / 1024;  // glds instructions per plane (1 KB each), dealt over the 8 waves
+  constexpr int ROWS = NWV * 16 * TT;
+  constexpr int DMA1 = W1B / 1024;  // 1-KB pieces per plane
   constexpr int DMA2 = W2B / 1024;
   static_assert(DMA1 * 1024 == W1B && DMA2 * 1024 == W2B, "DMA split");
   static_assert(RC % SW1 == 0 && (RB == 16 || RB == 8 || RB == 4), "swizzle");
   constexpr int BUF = PL * (W1B + W2B);  // one chunk of W1 and W2, double-buffered
   constexpr int LDS_W = 2 * BUF;
   __shared__ __attribute__((aligned(16))) char lds[LDS_W + (HID + C) * 4];
+  static_assert(NWV == 8 || NWV == 4, "8 or 4 waves");
   float* b1s = reinterpret_cast<float*>(lds + LDS_W);
   float* b2s = b1s + HID;
 
@@ -147,22 +144,21 @@ __global__ void __launch_bounds__(512) mlp_fused_kernel(MlpParams p) {
   const int g = lane >> 4;
   const long row0 = (long)blockIdx.x * ROWS + wave * 16 * TT;
 
-  // One chunk = PL x (DMA1 + DMA2) 1-KB pieces (W1 then W2 per plane), 8 waves x NST each.
+  // One chunk = PL x (DMA1 + DMA2) 1-KB pieces (W1 then W2 per plane), NWV waves x NST each.
   // Register-staged (global -> VGPR -> LDS): with LDS-DMA in flight hipcc drains it with
-  // vmcnt(0) before the GEMM-2 fragment reads, which serialised the prefetch.
+  // vmcnt(0) before the GEMM-2 fragment reads, which serialised the prefetch.  The packed
+  // chunk image (launch_mlp_pack) holds the LDS bytes in order, so piece k of wave w is the
+  // 1-KB block k NWV + w of the chunk, at the same offset in LDS.
   constexpr int NPIECE = PL * (DMA1 + DMA2);
-  constexpr int NST = NPIECE / 8;
-  constexpr int KPL = (DMA1 + DMA2) / 8;  // pieces per wave per plane
-  static_assert(KPL * 8 == DMA1 + DMA2, "pieces per wave");
-  // piece k of chunk jc from the packed chunk images (launch_mlp_pack: the LDS bytes in order)
+  constexpr int NST = NPIECE / NWV;
+  static_assert(NST * NWV == NPIECE, "pieces per wave");
   const char* wpk = static_cast<const char*>(p.wpack);
-  auto piece = [&](int jc, int k) {
-    return *reinterpret_cast<const uint4*>(wpk + (size_t)jc * BUF + mlp_piece_dst<PL, DMA1, KPL, W1B, W2B>(k, wave, lane));
-  };
+  auto pdst = [&](int k) { return (k * NWV + wave) * 1024 + lane * 16; };
+  auto piece = [&](int jc, int k) { return *reinterpret_cast<const uint4*>(wpk + (size_t)jc * BUF + pdst(k)); };
   StgList<0, NST> stg;
   stg.load([&](int k) { return piece(0, k); });
-  for (int i = tid; i < HID; i += 512) b1s[i] = p.b1[i];
-  for (int i = tid; i < C; i += 512) b2s[i] = p.b2[i];
+  for (int i = tid; i < HID; i += 64 * NWV) b1s[i] = p.b1[i];
+  for (int i = tid; i < C; i += 64 * NWV) b2s[i] = p.b2[i];
 
   // LayerNorm(norm2) of this wave's rows into GEMM 1's B fragments
   bf16x8 xb[TT][KS1][PL];
@@ -217,9 +213,7 @@ __global__ void __launch_bounds__(512) mlp_fused_kernel(MlpParams p) {
       if constexpr (X3) xb[tt][ks][PL - 1] = lo;
     }
   }
-  stg.store([&](int k, const uint4& v) {
-    *reinterpret_cast<uint4*>(lds + mlp_piece_dst<PL, DMA1, KPL, W1B, W2B>(k, wave, lane)) = v;
-  });
+  stg.store([&](int k, const uint4& v) { *reinterpret_cast<uint4*>(lds + pdst(k)) = v; });
   __syncthreads();
 
   floatx4 acc2[NCT][TT];
@@ -358,9 +352,7 @@ __global__ void __launch_bounds__(512) mlp_fused_kernel(MlpParams p) {
     // the other buffer was last read in chunk jc - 1, before the barrier that ended it
     if (more) {
       char* buf = lds + ((jc + 1) & 1) * BUF;
-      stg.store([&](int k, const uint4& v) {
-        *reinterpret_cast<uint4*>(buf + mlp_piece_dst<PL, DMA1, KPL, W1B, W2B>(k, wave, lane)) = v;
-      });
+      stg.store([&](int k, const uint4& v) { *reinterpret_cast<uint4*>(buf + pdst(k)) = v; });
     }
     __syncthreads();  // chunk jc + 1 visible; buffer jc & 1 free
   }
@@ -934,46 +926,52 @@ __global__ void __launch_bounds__(256) lngemm384_kernel(LnGemm384Params p) {
   }
 }
 
-// mlp_fused_kernel<C, TT, NC, PASSES>'s chunk images: chunk jc at jc * BUF, piece k of wave w
-// at the LDS offset the kernel stores it to, holding what mlp_piece_load gathers for it.
+// mlp_fused_kernel<C, TT, NC, PASSES, NWV>'s chunk images: chunk jc at jc * BUF in the LDS
+// byte order, piece rem of plane q holding what mlp_piece_load gathers for it (one 64-lane
+// block per piece; the kernel copies 1-KB blocks whatever its wave count).
 template <int C, int NC, int PASSES>
 struct MlpImage {
   static constexpr int PL = PASSES == 3 ? 2 : 1, RC = C / 8;
   static constexpr int SW1 = (RC % 16 == 0) ? 16 : ((RC % 8 == 0) ? 8 : 4), SH1 = SW1 == 16 ? 0 : 1;
   static constexpr int RB = NC / 8, SH2 = RB == 4 ? 1 : 0;
   static constexpr int W1B = NC * C * 2, W2B = C * NC * 2, DMA1 = W1B / 1024, DMA2 = W2B / 1024;
-  static constexpr int KPL = (DMA1 + DMA2) / 8, NST = PL * KPL, BUF = PL * (W1B + W2B), NCH = 4 * C / NC;
+  static constexpr int NPIECE = PL * (DMA1 + DMA2), BUF = PL * (W1B + W2B), NCH = 4 * C / NC;
 };
 template <int C, int NC, int PASSES>
-__global__ void mlp_pack_kernel(MlpParams p, char* __restrict__ out) {
+__global__ void __launch_bounds__(64) mlp_pack_kernel(MlpParams p, char* __restrict__ out) {
   using I = MlpImage<C, NC, PASSES>;
-  const int lane = threadIdx.x & 63;
-  const int wave = (threadIdx.x >> 6) & 7;
-  const int k = blockIdx.x % I::NST;
-  const int jc = blockIdx.x / I::NST;
-  const uint4 v = mlp_piece_load<C, NC, I::PL, I::DMA1, I::KPL, I::RC, I::SW1, I::SH1, I::RB, I::SH2>(p, jc, k, wave, lane);
-  *reinterpret_cast<uint4*>(out + (size_t)jc * I::BUF +
-                            mlp_piece_dst<I::PL, I::DMA1, I::KPL, I::W1B, I::W2B>(k, wave, lane)) = v;
+  const int lane = threadIdx.x;
+  const int P = blockIdx.x % I::NPIECE;
+  const int jc = blockIdx.x / I::NPIECE;
+  const int q = P / (I::DMA1 + I::DMA2);
+  const int rem = P - q * (I::DMA1 + I::DMA2);
+  const uint4 v = mlp_piece_load<C, NC, I::DMA1, I::RC, I::SW1, I::SH1, I::RB, I::SH2>(p, jc, q, rem, lane);
+  *reinterpret_cast<uint4*>(out + (size_t)jc * I::BUF + mlp_piece_dst<I::PL, I::DMA1, I::W1B, I::W2B>(q, rem, lane)) = v;
 }
 template <int C, int NC>
 void launch_pack_c(const MlpParams& p, void* out, hipStream_t s) {
   if (p.w1lo) {
     using I = MlpImage<C, NC, 3>;
-    mlp_pack_kernel<C, NC, 3><<<I::NCH * I::NST, 512, 0, s>>>(p, static_cast<char*>(out));
+    mlp_pack_kernel<C, NC, 3><<<I::NCH * I::NPIECE, 64, 0, s>>>(p, static_cast<char*>(out));
   } else {
     using I = MlpImage<C, NC, 1>;
-    mlp_pack_kernel<C, NC, 1><<<I::NCH * I::NST, 512, 0, s>>>(p, static_cast<char*>(out));
+    mlp_pack_kernel<C, NC, 1><<<I::NCH * I::NPIECE, 64, 0, s>>>(p, static_cast<char*>(out));
   }
 }
 
-template <int C, int TT, int NC>
+template <int C, int TT, int NC, int NWV = 8>
 void launch_mlp_c(const MlpParams& p, hipStream_t s) {
-  const unsigned grid = (unsigned)((p.M + 128 * TT - 1) / (128 * TT));
+  const unsigned grid = (unsigned)((p.M + 16 * NWV * TT - 1) / (16 * NWV * TT));
   if (p.w1lo && p.w2lo)
-    mlp_fused_kernel<C, TT, NC, 3><<<grid, 512, 0, s>>>(p);
+    mlp_fused_kernel<C, TT, NC, 3, NWV><<<grid, 64 * NWV, 0, s>>>(p);
   else
-    mlp_fused_kernel<C, TT, NC, 1><<<grid, 512, 0, s>>>(p);
+    mlp_fused_kernel<C, TT, NC, 1, NWV><<<grid, 64 * NWV, 0, s>>>(p);
 }
+// stage-1 MLP geometry (A/B builds: -DMOCR_S1_MLP_NWV=4 -> 4 waves, 32-unit chunks)
+#ifndef MOCR_S1_MLP_NWV
+#define MOCR_S1_MLP_NWV 8
+#endif
+constexpr int kS1MlpNC = MOCR_S1_MLP_NWV == 4 ? 32 : 64;
 
 }  // namespace
 
@@ -1015,7 +1013,7 @@ void launch_mlp_pack(const MlpParams& p, void* out, hipStream_t s) {
   if ((p.w1lo == nullptr) != (p.w2lo == nullptr) || !p.w1 || !p.w2 || !out)
     throw std::runtime_error("mlp_pack: planes");
   switch (p.C) {
-    case 96: launch_pack_c<96, 64>(p, out, s); break;
+    case 96: launch_pack_c<96, kS1MlpNC>(p, out, s); break;
     case 192: launch_pack_c<192, 32>(p, out, s); break;
     case 384: {
       const size_t img = (size_t)4 * 384 * 384 * 2 * (p.w1lo ? 2 : 1);  // W1's 48 chunk images
@@ -1035,7 +1033,7 @@ void launch_mlp_fused(const MlpParams& p, hipStream_t s) {
   switch (p.C) {
     // rows per wave 16 TT and hidden chunk NC measured best (TT = 1 at C = 96: 514 vs 420 us
     // per s1 block; TT = 2 at C = 192 spills)
-    case 96: launch_mlp_c<96, 2, 64>(p, s); break;  // NC: launch_mlp_pack's chunks
+    case 96: launch_mlp_c<96, 2, kS1MlpNC, MOCR_S1_MLP_NWV>(p, s); break;  // NC: launch_mlp_pack's chunks
     case 192: launch_mlp_c<192, 1, 32>(p, s); break;
     case 384: {
       const unsigned grid = (unsigned)((p.M + 127) / 128);
