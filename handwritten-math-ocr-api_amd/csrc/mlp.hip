@@ -967,9 +967,13 @@ void launch_mlp_c(const MlpParams& p, hipStream_t s) {
   else
     mlp_fused_kernel<C, TT, NC, 1, NWV><<<grid, 64 * NWV, 0, s>>>(p);
 }
-// stage-1 MLP geometry (A/B builds: -DMOCR_S1_MLP_NWV=4 -> 4 waves, 32-unit chunks)
+// stage-1 MLP geometry: 4 waves (128 rows) per workgroup with 32-unit chunks (49 KB of LDS,
+// 152 VGPRs: three workgroups per CU, whose LayerNorm prologues and residual epilogues
+// overlap the others' chunk loops) instead of 8 waves with 64-unit chunks (100 KB, 256
+// VGPRs, one per CU): 5.30-5.39 vs 5.72-5.75 ms per 512-image encode (profiles/r05/r06f).
+// A/B builds: -DMOCR_S1_MLP_NWV=8
 #ifndef MOCR_S1_MLP_NWV
-#define MOCR_S1_MLP_NWV 8
+#define MOCR_S1_MLP_NWV 4
 #endif
 constexpr int kS1MlpNC = MOCR_S1_MLP_NWV == 4 ? 32 : 64;
 

@@ -969,12 +969,16 @@ void launch_c(const SwinAttnParams& p, hipStream_t s) {
     swin_attn_kernel<C, 1, OCC, WPB><<<grid, 2 * C * WPB, 0, s>>>(p);
 }
 // windows per workgroup (A/B builds: tools/build_variant.sh DIR -DMOCR_S1_WPB=2); at C = 192
-// two windows need 3 waves per SIMD (12 waves per workgroup)
+// two windows need 3 waves per SIMD (12 waves per workgroup).  Measured per 512-image encode
+// (two launches, profiles/r05/r06f/ops_*.log): C = 192 3.83-3.86 ms at two windows vs
+// 4.77 at one (590 KB of W_qkv + W_proj per window, read once per window pair from L2 /
+// L1); C = 96 6.86-6.90 ms at two vs 4.79 at one (147 KB per window; four 3-wave
+// workgroups per CU overlap better than two 6-wave ones)
 #ifndef MOCR_S1_WPB
 #define MOCR_S1_WPB 1
 #endif
 #ifndef MOCR_S2_WPB
-#define MOCR_S2_WPB 1
+#define MOCR_S2_WPB 2
 #endif
 
 // waves per SIMD the register allocation targets: 3 at C = 96 (534 vs 651 us per s1
