@@ -104,7 +104,7 @@ __device__ __forceinline__ int mlp_piece_dst(int q, int rem, int lane) {
   return in1 ? q * W1B + sl * 16 : PL * W1B + q * W2B + sl * 16;
 }
 
-template <int C, int TT, int NC, int PASSES, int NWV = 8>
+template <int C, int TT, int NC, int PASSES, int NWV = 8, int NBUF = 2>
 __global__ void __launch_bounds__(64 * NWV) mlp_fused_kernel(MlpParams p) {
   constexpr bool X3 = PASSES == 3;
   constexpr int PL = X3 ? 2 : 1;
@@ -131,7 +131,9 @@ __global__ void __launch_bounds__(64 * NWV) mlp_fused_kernel(MlpParams p) {
   static_assert(DMA1 * 1024 == W1B && DMA2 * 1024 == W2B, "DMA split");
   static_assert(RC % SW1 == 0 && (RB == 16 || RB == 8 || RB == 4), "swizzle");
   constexpr int BUF = PL * (W1B + W2B);  // one chunk of W1 and W2, double-buffered
-  constexpr int LDS_W = 2 * BUF;
+  // NBUF = 2: chunk jc + 1 is stored into the other buffer while chunk jc is read; NBUF = 1
+  // (half the LDS: two 4-wave workgroups per CU at C = 192): stored after a barrier
+  constexpr int LDS_W = NBUF * BUF;
   __shared__ __attribute__((aligned(16))) char lds[LDS_W + (HID + C) * 4];
   static_assert(NWV == 8 || NWV == 4, "8 or 4 waves");
   float* b1s = reinterpret_cast<float*>(lds + LDS_W);
@@ -239,7 +241,7 @@ __global__ void __launch_bounds__(64 * NWV) mlp_fused_kernel(MlpParams p) {
     if (more) {
       stg.load([&](int k) { return piece(jc + 1, k); });
     }
-    const char* w1s = lds + (jc & 1) * BUF;
+    const char* w1s = lds + (NBUF == 2 ? (jc & 1) * BUF : 0);
     const char* w2s = w1s + PL * W1B;
     // GEMM 1: hidden^T [NC x 16TT] = W1[chunk] . LN(x)^T
     floatx4 acc1[NH][TT];
@@ -351,7 +353,8 @@ __global__ void __launch_bounds__(64 * NWV) mlp_fused_kernel(MlpParams p) {
     }
     // the other buffer was last read in chunk jc - 1, before the barrier that ended it
     if (more) {
-      char* buf = lds + ((jc + 1) & 1) * BUF;
+      if constexpr (NBUF == 1) __syncthreads();  // every wave is done with the one buffer
+      char* buf = lds + (NBUF == 2 ? ((jc + 1) & 1) * BUF : 0);
       stg.store([&](int k, const uint4& v) { *reinterpret_cast<uint4*>(buf + pdst(k)) = v; });
     }
     __syncthreads();  // chunk jc + 1 visible; buffer jc & 1 free
@@ -959,13 +962,13 @@ void launch_pack_c(const MlpParams& p, void* out, hipStream_t s) {
   }
 }
 
-template <int C, int TT, int NC, int NWV = 8>
+template <int C, int TT, int NC, int NWV = 8, int NBUF = 2>
 void launch_mlp_c(const MlpParams& p, hipStream_t s) {
   const unsigned grid = (unsigned)((p.M + 16 * NWV * TT - 1) / (16 * NWV * TT));
   if (p.w1lo && p.w2lo)
-    mlp_fused_kernel<C, TT, NC, 3, NWV><<<grid, 64 * NWV, 0, s>>>(p);
+    mlp_fused_kernel<C, TT, NC, 3, NWV, NBUF><<<grid, 64 * NWV, 0, s>>>(p);
   else
-    mlp_fused_kernel<C, TT, NC, 1, NWV><<<grid, 64 * NWV, 0, s>>>(p);
+    mlp_fused_kernel<C, TT, NC, 1, NWV, NBUF><<<grid, 64 * NWV, 0, s>>>(p);
 }
 // stage-1 MLP geometry: 4 waves (128 rows) per workgroup with 32-unit chunks (49 KB of LDS,
 // 152 VGPRs: three workgroups per CU, whose LayerNorm prologues and residual epilogues
@@ -974,6 +977,10 @@ void launch_mlp_c(const MlpParams& p, hipStream_t s) {
 // A/B builds: -DMOCR_S1_MLP_NWV=8
 #ifndef MOCR_S1_MLP_NWV
 #define MOCR_S1_MLP_NWV 4
+#endif
+// stage 2 (A/B builds: -DMOCR_S2_MLP_NWV=4: 4-wave workgroups of 64 rows, one LDS buffer)
+#ifndef MOCR_S2_MLP_NWV
+#define MOCR_S2_MLP_NWV 8
 #endif
 constexpr int kS1MlpNC = MOCR_S1_MLP_NWV == 4 ? 32 : 64;
 
@@ -1038,7 +1045,7 @@ void launch_mlp_fused(const MlpParams& p, hipStream_t s) {
     // rows per wave 16 TT and hidden chunk NC measured best (TT = 1 at C = 96: 514 vs 420 us
     // per s1 block; TT = 2 at C = 192 spills)
     case 96: launch_mlp_c<96, 2, kS1MlpNC, MOCR_S1_MLP_NWV>(p, s); break;  // NC: launch_mlp_pack's chunks
-    case 192: launch_mlp_c<192, 1, 32>(p, s); break;
+    case 192: launch_mlp_c<192, 1, 32, MOCR_S2_MLP_NWV, MOCR_S2_MLP_NWV == 4 ? 1 : 2>(p, s); break;
     case 384: {
       const unsigned grid = (unsigned)((p.M + 127) / 128);
       if (p.w1lo)

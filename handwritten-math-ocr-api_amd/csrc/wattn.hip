@@ -393,7 +393,10 @@ __global__ void __launch_bounds__(2 * C * WPB) __attribute__((amdgpu_waves_per_e
   for (int t = 0; t < 4; ++t) ap[0][t] = ap[1][t] = floatx4{0.f, 0.f, 0.f, 0.f};
   __builtin_amdgcn_s_setprio(1);
   bf16x8 wa[2][2];
-#pragma unroll
+  // at C = 192 (6 heads) a full unroll hoists every k-step's weight loads and spilled 76
+  // bytes per lane at 3 waves per SIMD; by 2: none
+  constexpr int PU = C == 192 ? 2 : HEADS;
+#pragma unroll PU
   for (int hh = 0; hh < HEADS; ++hh) {
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
