@@ -28,7 +28,27 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+#ifndef MOCR_GELU_728
+#define MOCR_GELU_728 0
+#endif
 __device__ __forceinline__ float gelu_erf_fast(float x) {  // gemm.hip gelu_fast (A&S 7.1.26)
+  if constexpr (MOCR_GELU_728) {
+    // A&S 7.1.28: erf(z) = 1 - (1 + a1 z + ... + a6 z^6)^-16, |error| <= 3e-7: one
+    // reciprocal and no exp (7.1.26 needs both); GELU's absolute error <= 5e-7
+    const float z = fabsf(x) * 0.70710678118654752440f;
+    float p = fmaf(4.30638e-5f, z, 2.765672e-4f);
+    p = fmaf(p, z, 1.520143e-4f);
+    p = fmaf(p, z, 9.2705272e-3f);
+    p = fmaf(p, z, 4.22820123e-2f);
+    p = fmaf(p, z, 7.05230784e-2f);
+    p = fmaf(p, z, 1.0f);
+    p = p * p;
+    p = p * p;
+    p = p * p;
+    p = p * p;
+    const float e = 1.0f - __builtin_amdgcn_rcpf(p);
+    return x * 0.5f * (1.0f + copysignf(e, x));
+  }
   const float z = fabsf(x) * 0.70710678118654752440f;
   const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
   float poly = fmaf(1.061405429f, t, -1.453152027f);
