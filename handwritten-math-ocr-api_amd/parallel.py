@@ -104,6 +104,30 @@ class RcclGroup:
             pass
 
 
+def global_stop(ids, eos: int):
+    """SURVEY.md §8(e) option 2: the reference's batch-global stop over the WHOLE sharded
+    batch (``src/inference.py:18-25``: the loop ends after the step at which every row of
+    the batch has produced EOS; finished rows keep generating until then).
+
+    ``ids``: the gathered ``[B, S+1]`` token streams of every shard, each shard decoded with
+    ``stop="none"`` (column 0 = sos, step t's token in column t+1).  A row's tokens up to
+    any step do not depend on when the loop ends, so the global decode is the first
+    ``n + 1`` columns, where ``n - 1`` is the latest first-EOS step over all rows (``n = S``
+    when some row never produced EOS).  No collective beyond the all-gather the ids already
+    went through: every rank computes the same ``n`` from the same gathered tensor.
+    Returns ``(ids[:, :n + 1], n)``; equal, columns and step count, to one process decoding
+    the whole batch with ``stop="batch"``."""
+    import numpy as np
+    a = ids.cpu().numpy() if hasattr(ids, "cpu") else np.asarray(ids)
+    S = a.shape[1] - 1
+    hit = a[:, 1:] == eos
+    if a.shape[0] == 0 or not hit.any(axis=1).all():
+        n = S
+    else:
+        n = int(hit.argmax(axis=1).max()) + 1
+    return ids[:, :n + 1], n
+
+
 def gather_ids_host(ids_local, world: int, group=None):
     """All-gather equal-shaped per-rank CPU id tensors over a host process group (gloo)
     and concatenate them in rank order (multi-process CPU tests)."""

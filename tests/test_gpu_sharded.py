@@ -47,7 +47,10 @@ def _worker(rank, world, port, q, stop="none"):
         eng.load_weights(apply_eos_boost(pkg.synth.make_weights(m["seed"], m["variant"]), m["eos_boost"]))
         eng.encode(imgs)
         steps = g["ids"].shape[1] - 1
-        res = eng.decode(max_steps=steps if stop == "none" else m["steps"], stop=stop)
+        if stop == "global":  # SURVEY §8(e) option 2: decode without stopping, cut after the gather
+            res = eng.decode(max_steps=m["steps"], stop="none")
+        else:
+            res = eng.decode(max_steps=steps if stop == "none" else m["steps"], stop=stop)
         eng.close()
         # a shard under the batch stop ends when its own rows have all finished (DESIGN.md
         # §6): pad its ids to the fixture's width for the gather, and report its step count
@@ -112,6 +115,18 @@ def test_two_shards_batch_stop_each_shard_stops_on_its_own(pkg, golden):
     # the detokenised strings (cut at EOS) are the fixture's
     vocab, idx2char = pkg.synth.synthetic_vocab()
     assert [pkg.utils.detokenize(r.tolist(), idx2char) for r in out] == g["meta"]["strings"]
+
+
+def test_two_shards_global_stop_equals_one_process(pkg, golden):
+    """SURVEY §8(e) option 2: each shard decodes all 150 steps without stopping, the ids are
+    gathered, and `parallel.global_stop` cuts them after the step at which the last row of
+    the whole batch produced EOS: every column, post-EOS tokens included, and the step
+    count equal the fixture's single-process batch-stop decode."""
+    g = golden("g96x320_b4_eos")
+    gathered, _ = _run_shards("global")
+    cut, n = pkg.parallel.global_stop(gathered, pkg.synth.EOS_ID)
+    assert n == g["ids"].shape[1] - 1
+    np.testing.assert_array_equal(cut, g["ids"])
 
 
 def test_rccl_group_gather_one_rank(pkg):

@@ -175,3 +175,22 @@ def test_replica_pool_imap_order_and_errors(pkg):
         for v in pool.imap(bad, range(8)):
             got.append(v)
     assert got == [0, 1, 2, 3]
+
+
+def test_global_stop_over_shards(pkg):
+    """SURVEY §8(e) option 2 on gathered ids: the batch stops after the step at which the
+    last row produced its first EOS; a row that never does keeps the full width."""
+    import numpy as np
+    eos = pkg.synth.EOS_ID
+    ids = np.full((3, 9), 7, np.int32)
+    ids[:, 0] = pkg.synth.SOS_ID
+    ids[0, 3] = eos  # step 2
+    ids[1, 6] = eos  # step 5 (the global stop)
+    ids[2, 2] = eos  # step 1, then post-EOS tokens
+    ids[2, 4] = eos
+    out, n = pkg.parallel.global_stop(ids, eos)
+    assert n == 6 and out.shape == (3, 7)
+    np.testing.assert_array_equal(out, ids[:, :7])
+    ids[1, 6] = 7  # row 1 never finishes: no stop
+    out, n = pkg.parallel.global_stop(ids, eos)
+    assert n == 8 and out.shape == (3, 9)
