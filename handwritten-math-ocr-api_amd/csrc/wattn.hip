@@ -191,33 +191,46 @@ __global__ void __launch_bounds__(2 * C * WPB) __attribute__((amdgpu_waves_per_e
     if constexpr (X3) f[1] = *reinterpret_cast<const bf16x8*>(lds + XB + off);
   };
   // acc[f][t] = W[row0 + 16f + j16, :] . LN^T (features x tokens)
-  auto gemm_t = [&](int row0, floatx4(&acc)[2][4]) {
+  // the weight fragments of k-step ks + 1 are loaded while the MFMAs of ks run (a register
+  // double buffer; the scheduling barrier keeps hipcc from sinking the loads to their use,
+  // where each one waited out its whole L2 round trip)
+  auto wload = [&](int row0, int ks, bf16x8(&w)[2][2]) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      if constexpr (MOCR_WATTN_PROBE == 5) w[f][0] = w[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)ks, 1u, 2u, 3u});
+      else if (MOCR_WATTN_PROBE != 6 || (ks & 1) == 0) wfm(row0, f, ks, w[f]);
+    }
+  };
+  // PRE: the double buffer (the k^T GEMM; the q^T GEMM runs with k and v live and keeps
+  // one buffer: two spilled)
+  auto gemm_t = [&](int row0, floatx4(&acc)[2][4], auto pre) {
+    constexpr bool PRE = decltype(pre)::value;
 #pragma unroll
     for (int f = 0; f < 2; ++f)
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[f][t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 w[2][2];
+    bf16x8 w[PRE ? 2 : 1][2][2];
+    wload(row0, 0, w[0]);
 #pragma unroll
     for (int ks = 0; ks < HEADS; ++ks) {
-#pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        if constexpr (MOCR_WATTN_PROBE == 5) w[f][0] = w[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)ks, 1u, 2u, 3u});
-        else if (MOCR_WATTN_PROBE != 6 || (ks & 1) == 0) wfm(row0, f, ks, w[f]);
-      }
+      if (PRE && ks + 1 < HEADS) wload(row0, ks + 1, w[(ks + 1) & (PRE ? 1 : 0)]);
+      else if (!PRE && ks > 0) wload(row0, ks, w[0]);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         bf16x8 xf[2];
         xfrag(ks, t, xf);
 #pragma unroll
-        for (int f = 0; f < 2; ++f) acc[f][t] = MOCR_WATTN_PROBE == 2 ? acc[f][t] + xf[0][0] : mma<X3>(w[f], xf, acc[f][t]);
+        for (int f = 0; f < 2; ++f)
+          acc[f][t] = MOCR_WATTN_PROBE == 2 ? acc[f][t] + xf[0][0] : mma<X3>(w[ks & (PRE ? 1 : 0)][f], xf, acc[f][t]);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
   bf16x8 kf[4][2], vf[2][2][2], qf4[4][2];
   __builtin_amdgcn_s_setprio(1);
   {
     floatx4 acc[2][4];
-    gemm_t(C + 32 * h, acc);
+    gemm_t(C + 32 * h, acc, std::true_type{});
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
       float x[8];
@@ -237,21 +250,20 @@ __global__ void __launch_bounds__(2 * C * WPB) __attribute__((amdgpu_waves_per_e
     floatx4 acc[4][2];
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[t][0] = acc[t][1] = floatx4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 w[2][2];
+    bf16x8 w[2][2][2];
+    wload(2 * C + 32 * h, 0, w[0]);
 #pragma unroll
     for (int ks = 0; ks < HEADS; ++ks) {
-#pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        if constexpr (MOCR_WATTN_PROBE == 5) w[f][0] = w[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)ks, 1u, 2u, 3u});
-        else if (MOCR_WATTN_PROBE != 6 || (ks & 1) == 0) wfm(2 * C + 32 * h, f, ks, w[f]);
-      }
+      if (ks + 1 < HEADS) wload(2 * C + 32 * h, ks + 1, w[(ks + 1) & 1]);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         bf16x8 xf[2];
         xfrag(ks, t, xf);
 #pragma unroll
-        for (int f = 0; f < 2; ++f) acc[t][f] = MOCR_WATTN_PROBE == 2 ? acc[t][f] + xf[0][0] : mma<X3>(xf, w[f], acc[t][f]);
+        for (int f = 0; f < 2; ++f)
+          acc[t][f] = MOCR_WATTN_PROBE == 2 ? acc[t][f] + xf[0][0] : mma<X3>(xf, w[ks & 1][f], acc[t][f]);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) {
@@ -271,7 +283,7 @@ __global__ void __launch_bounds__(2 * C * WPB) __attribute__((amdgpu_waves_per_e
   __builtin_amdgcn_sched_barrier(0);
   {
     floatx4 acc[2][4];
-    gemm_t(32 * h, acc);
+    gemm_t(32 * h, acc, std::false_type{});
     const float scale = 0.17677669529663687f;  // 32 ** -0.5
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) {
@@ -392,12 +404,9 @@ __global__ void __launch_bounds__(2 * C * WPB) __attribute__((amdgpu_waves_per_e
 #pragma unroll
   for (int t = 0; t < 4; ++t) ap[0][t] = ap[1][t] = floatx4{0.f, 0.f, 0.f, 0.f};
   __builtin_amdgcn_s_setprio(1);
-  bf16x8 wa[2][2];
-  // at C = 192 (6 heads) a full unroll hoists every k-step's weight loads and spilled 76
-  // bytes per lane at 3 waves per SIMD; by 2: none
-  constexpr int PU = C == 192 ? 2 : HEADS;
-#pragma unroll PU
-  for (int hh = 0; hh < HEADS; ++hh) {
+  // W_proj fragments one k-step ahead, as the qkv GEMMs.  At C = 192 (6 heads) a full
+  // unroll hoisted every k-step's weight loads and spilled at 3 waves per SIMD: by 2
+  auto pload = [&](int hh, bf16x8(&wa)[2][2]) {
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
       if constexpr (MOCR_WATTN_PROBE == 5) wa[f][0] = wa[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)hh, 1u, 2u, 3u});
@@ -407,6 +416,13 @@ __global__ void __launch_bounds__(2 * C * WPB) __attribute__((amdgpu_waves_per_e
         if constexpr (X3) wa[f][1] = wpl[o];
       }
     }
+  };
+  bf16x8 wa[2][2][2];
+  pload(0, wa[0]);
+  constexpr int PU = C == 192 ? 2 : HEADS;
+#pragma unroll PU
+  for (int hh = 0; hh < HEADS; ++hh) {
+    if (hh + 1 < HEADS) pload(hh + 1, wa[(hh + 1) & 1]);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       bf16x8 of[2];
@@ -414,8 +430,10 @@ __global__ void __launch_bounds__(2 * C * WPB) __attribute__((amdgpu_waves_per_e
       of[0] = *reinterpret_cast<const bf16x8*>(lds + off);
       if constexpr (X3) of[1] = *reinterpret_cast<const bf16x8*>(lds + XB + off);
 #pragma unroll
-      for (int f = 0; f < 2; ++f) ap[f][t] = MOCR_WATTN_PROBE == 4 ? ap[f][t] + of[0][0] : mma<X3>(wa[f], of, ap[f][t]);
+      for (int f = 0; f < 2; ++f)
+        ap[f][t] = MOCR_WATTN_PROBE == 4 ? ap[f][t] + of[0][0] : mma<X3>(wa[hh & 1][f], of, ap[f][t]);
     }
+    __builtin_amdgcn_sched_barrier(0);
   }
   __builtin_amdgcn_s_setprio(0);
 #pragma unroll
@@ -631,27 +649,34 @@ swin_attn_noproj_kernel(SwinAttnParams p) {
     f[0] = *reinterpret_cast<const bf16x8*>(lds + off);
     if constexpr (X3) f[1] = *reinterpret_cast<const bf16x8*>(lds + XB + off);
   };
+  // weight fragments of k-step ks + 1 loaded while the MFMAs of ks run (swin_attn_kernel)
+  auto wload = [&](int row0, int ks, bf16x8(&w)[2][2]) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      if constexpr (MOCR_WATTN_PROBE == 5) w[f][0] = w[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)ks, 1u, 2u, 3u});
+      else if (MOCR_WATTN_PROBE != 6 || (ks & 1) == 0) wfm(row0, f, ks, w[f]);
+    }
+  };
   // acc[f][t] = W[row0 + 16f + j16, :] . LN^T (features x tokens)
   auto gemm_t = [&](int row0, floatx4(&acc)[2][4]) {
 #pragma unroll
     for (int f = 0; f < 2; ++f)
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[f][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 w[2][2][2];
+    wload(row0, 0, w[0]);
 #pragma unroll KU
     for (int ks = 0; ks < HEADS; ++ks) {
-      bf16x8 w[2][2];
-#pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        if constexpr (MOCR_WATTN_PROBE == 5) w[f][0] = w[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)ks, 1u, 2u, 3u});
-        else if (MOCR_WATTN_PROBE != 6 || (ks & 1) == 0) wfm(row0, f, ks, w[f]);
-      }
+      if (ks + 1 < HEADS) wload(row0, ks + 1, w[(ks + 1) & 1]);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         bf16x8 xf[2];
         xfrag(ks, t, xf);
 #pragma unroll
-        for (int f = 0; f < 2; ++f) acc[f][t] = MOCR_WATTN_PROBE == 2 ? acc[f][t] + xf[0][0] : mma<X3>(w[f], xf, acc[f][t]);
+        for (int f = 0; f < 2; ++f)
+          acc[f][t] = MOCR_WATTN_PROBE == 2 ? acc[f][t] + xf[0][0] : mma<X3>(w[ks & 1][f], xf, acc[f][t]);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 
@@ -687,18 +712,19 @@ swin_attn_noproj_kernel(SwinAttnParams p) {
       floatx4 acc[4][2];
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[t][0] = acc[t][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+      bf16x8 w[2][2][2];
+      wload(2 * C + 32 * h, 0, w[0]);
 #pragma unroll KU
       for (int ks = 0; ks < HEADS; ++ks) {
-        bf16x8 w[2][2];
-#pragma unroll
-        for (int f = 0; f < 2; ++f) wfm(2 * C + 32 * h, f, ks, w[f]);
+        if (ks + 1 < HEADS) wload(2 * C + 32 * h, ks + 1, w[(ks + 1) & 1]);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           bf16x8 xf[2];
           xfrag(ks, t, xf);
 #pragma unroll
-          for (int f = 0; f < 2; ++f) acc[t][f] = mma<X3>(xf, w[f], acc[t][f]);
+          for (int f = 0; f < 2; ++f) acc[t][f] = mma<X3>(xf, w[ks & 1][f], acc[t][f]);
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
