@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-box A/B of two libmathocr.so builds on decode-only and full-pipeline capacity
 # (tools/pipeline_probe.py, 4 replicas; decode-only also at 1 replica), alternating A B A B.
-#   tools/gpu_ab_decode.sh TAG LIB_A LIB_B
+#   tools/sessions/gpu_ab_decode.sh TAG LIB_A LIB_B
 mkdir -p gpurun_out
 O=gpurun_out/abd_$1.log
 : > $O

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-box A/B of an encoder-kernel variant build: bitwise stage maps (tests/probes/stage_diff.py),
 # per-op HIP-event times (tools/op_times.py) and the bench pipeline (tools/pipeline_probe.py).
-#   tools/gpu_ab_encoder_op.sh TAG LIB_A LIB_B FILTER     (e.g. FILTER=s3.)
+#   tools/sessions/gpu_ab_encoder_op.sh TAG LIB_A LIB_B FILTER     (e.g. FILTER=s3.)
 mkdir -p gpurun_out
 TAG=$1; A=$2; B=$3; F=${4:-s3.}
 O=gpurun_out/ab_$TAG.log

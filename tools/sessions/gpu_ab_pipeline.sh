@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-box A/B of two libmathocr.so builds on the bench pipeline (tools/pipeline_probe.py):
-#   tools/gpu_ab_pipeline.sh TAG LIB_A LIB_B   (alternating A B A B, encode-only and both)
+#   tools/sessions/gpu_ab_pipeline.sh TAG LIB_A LIB_B   (alternating A B A B, encode-only and both)
 mkdir -p gpurun_out
 O=gpurun_out/ab_$1.log
 : > $O

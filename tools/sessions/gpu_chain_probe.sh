@@ -1,6 +1,6 @@
 #!/bin/bash
 # Decode capacity by rows per chain x chains, and rocprofv3 kernel stats of one 64-row and
-# one 256-row chain (tools/decode_chain_probe.py).  Usage: tools/gpu_chain_probe.sh TAG
+# one 256-row chain (tools/decode_chain_probe.py).  Usage: tools/sessions/gpu_chain_probe.sh TAG
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/${1:-chain}

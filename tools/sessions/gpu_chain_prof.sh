@@ -1,5 +1,5 @@
 #!/bin/bash
-# rocprofv3 kernel stats of one decode chain per row count.  Usage: tools/gpu_chain_prof.sh TAG ROWS...
+# rocprofv3 kernel stats of one decode chain per row count.  Usage: tools/sessions/gpu_chain_prof.sh TAG ROWS...
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/${1:-cp}

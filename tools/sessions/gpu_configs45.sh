@@ -1,6 +1,6 @@
 #!/bin/bash
 # BASELINE configs 5 (ResNet18-trans, B = 64) and 4 (beam 4, B = 32, 256 tokens) on the
-# current tree.  Usage: tools/gpu_configs45.sh TAG
+# current tree.  Usage: tools/sessions/gpu_configs45.sh TAG
 set -o pipefail
 mkdir -p gpurun_out
 T=${1:-c45}

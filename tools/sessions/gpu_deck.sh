@@ -1,5 +1,5 @@
 #!/bin/bash
-# Decode-kernel microbenchmark under environment variants: tools/gpu_deck.sh TAG "ENV=.." ...
+# Decode-kernel microbenchmark under environment variants: tools/sessions/gpu_deck.sh TAG "ENV=.." ...
 set -e
 mkdir -p gpurun_out
 TAG=$1

@@ -1,5 +1,5 @@
 #!/bin/bash
-# GEMM dispatch A/B on the encoder shapes: tools/gpu_gemm_ab.sh TAG
+# GEMM dispatch A/B on the encoder shapes: tools/sessions/gpu_gemm_ab.sh TAG
 # (gemm_bench: kernel -1 = the dispatch before the 288-row tiles, 0 = the current dispatch)
 mkdir -p gpurun_out
 TAG=${1:-ab}

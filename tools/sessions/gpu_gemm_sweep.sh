@@ -1,5 +1,5 @@
 #!/bin/bash
-# GEMM microbenchmark over shapes: tools/gpu_gemm_sweep.sh TAG "M N K passes epi" ...
+# GEMM microbenchmark over shapes: tools/sessions/gpu_gemm_sweep.sh TAG "M N K passes epi" ...
 set -e
 mkdir -p gpurun_out
 TAG=$1

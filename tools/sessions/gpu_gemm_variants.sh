@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same GEMM shapes through gemm_bench binaries linked against variant libraries:
-# tools/gpu_gemm_variants.sh TAG VARIANT...   (tools/gemm_bench_VARIANT; "base" = tools/gemm_bench)
+# tools/sessions/gpu_gemm_variants.sh TAG VARIANT...   (tools/gemm_bench_VARIANT; "base" = tools/gemm_bench)
 mkdir -p gpurun_out
 TAG=$1; shift
 O=gpurun_out/gemm_var_$TAG.log

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Stage-3 fused MLP: encoder parity (every bf16 variant) then per-op times fused vs
-# unfused at B = 64 and 256.  Usage: tools/gpu_mlp384.sh TAG
+# unfused at B = 64 and 256.  Usage: tools/sessions/gpu_mlp384.sh TAG
 set -o pipefail
 mkdir -p gpurun_out
 T=${1:-mlp384}

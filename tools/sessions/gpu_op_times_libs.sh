@@ -1,6 +1,6 @@
 #!/bin/bash
 # tools/op_times.py over several libmathocr.so builds, alternating twice:
-#   tools/gpu_op_times_libs.sh TAG FILTER LIB...
+#   tools/sessions/gpu_op_times_libs.sh TAG FILTER LIB...
 mkdir -p gpurun_out
 TAG=$1; F=$2; shift 2
 O=gpurun_out/optimes_$TAG.log

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Encode-only / decode-only / both capacity vs replicas (tools/pipeline_probe.py): tools/gpu_probe.sh TAG MODES R...
+# Encode-only / decode-only / both capacity vs replicas (tools/pipeline_probe.py): tools/sessions/gpu_probe.sh TAG MODES R...
 set -e
 mkdir -p gpurun_out
 TAG=$1

@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU test suite + smoke + default bench, each under its own time limit; the first
-# failure ends the script.  Usage: tools/gpu_quick.sh TAG
+# failure ends the script.  Usage: tools/sessions/gpu_quick.sh TAG
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/${1:-quick}; mkdir -p $O

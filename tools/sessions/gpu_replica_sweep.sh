@@ -1,6 +1,6 @@
 #!/bin/bash
 # Replica-count sweep of the bench pipeline on the current build (both halves, 24 batches):
-#   tools/gpu_replica_sweep.sh TAG
+#   tools/sessions/gpu_replica_sweep.sh TAG
 mkdir -p gpurun_out
 O=gpurun_out/replicas_$1.log
 : > $O

@@ -4,7 +4,7 @@
 #   GPU test suite -> smoke -> headline bench (BASELINE config 2) -> rocprofv3 kernel
 #   stats of a short bench -> FETCH_SIZE / WRITE_SIZE PMC passes of one encode + 8 greedy
 #   steps (tools/pmc_traffic.py maps them to kernel classes).
-# Usage: tools/gpu_round.sh TAG [notests]
+# Usage: tools/sessions/gpu_round.sh TAG [notests]
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1

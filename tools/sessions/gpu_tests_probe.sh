@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU test suite, then the decode chain probe.  Usage: tools/gpu_tests_probe.sh TAG [probe args]
+# GPU test suite, then the decode chain probe.  Usage: tools/sessions/gpu_tests_probe.sh TAG [probe args]
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/${1:-tp}
