@@ -297,6 +297,9 @@ __device__ unsigned long long g_attn_ts[8192 * 8];
 // head, key) over its 32 values (the key's scale multiplies its score, the value's its
 // softmax weight), the newest key / value quantised here by the same rule.
 // NW waves (8 key rows each per pass; the selection runs on all 64 NW threads).
+#ifndef MOCR_XATTN_PROBE
+#define MOCR_XATTN_PROBE 0
+#endif
 template <bool SELF, bool ZS, bool SEL, int NIT, int KVF, int NW, bool SLOT = false>
 __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   MOCR_ATS(0, __builtin_amdgcn_s_memrealtime());
@@ -325,7 +328,9 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   static_assert(!SLOT || (SELF && !SEL), "slot tables: the self-attention of beam hypotheses");
   // the K/V row: this decoder row, its image's memory row (cross-attention of beam
   // hypotheses: mem_div of them per image), or per key its slot row (SLOT, below)
-  const int mb = SELF ? b : (p.mem_div > 1 ? b / p.mem_div : b);
+  // MOCR_XATTN_PROBE (timing probe, wrong results): every row's cross-attention reads
+  // memory row 0's K/V, which then stays in L2 (what the K/V stream costs in the pipeline)
+  const int mb = SELF ? b : (MOCR_XATTN_PROBE ? 0 : (p.mem_div > 1 ? b / p.mem_div : b));
   auto row_base = [&](int r) -> size_t {
     return KVF ? (size_t)r * p.f24_b + (size_t)h * p.f24_h + li * 4 : (size_t)r * p.kv_b_stride + cc;
   };
