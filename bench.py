@@ -129,6 +129,23 @@ def warm_replicas(pool, step):
     return warmed
 
 
+class stdout_to_stderr:
+    """Route file descriptor 1 to 2 for the block: gloo's connect messages ("[Gloo] Rank r is
+    connected to ...") are written to the process's stdout by the C++ library, and the
+    driver reads rank 0's stdout as the ONE JSON line of the run."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
 def free_port():
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
@@ -313,7 +330,9 @@ def main():
     rccl_ranks = None
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("gloo")  # host-side control only
+        with stdout_to_stderr():
+            dist.init_process_group("gloo")  # host-side control only
+            dist.barrier()  # every rank connected (gloo prints as it connects)
         if shared:
             # RCCL refuses two ranks on one device: the 33 KB token streams go over the host
             # group instead (only on a box with fewer GPUs than ranks; tests/test_gpu_sharded.py)
@@ -337,7 +356,8 @@ def main():
     if gather.startswith("rccl"):
         # after the engines: their HIP streams take the process's first hardware queues
         # (GPU_MAX_HW_QUEUES = 4), the group's stream and RCCL's own come after them
-        grp = pkg.parallel.RcclGroup(world, rank, local)  # RCCL inside libmathocr.so
+        with stdout_to_stderr():
+            grp = pkg.parallel.RcclGroup(world, rank, local)  # RCCL inside libmathocr.so
         rccl_ranks = grp.size()  # ncclCommCount
         if rccl_ranks != world:
             raise SystemExit(f"RCCL communicator counts {rccl_ranks} ranks, WORLD_SIZE is {world}")

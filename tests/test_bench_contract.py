@@ -175,3 +175,37 @@ def test_gpus8_without_launcher_starts_eight_ranks(bench, monkeypatch):
     a = bench.parse()
     assert bench.launch_if_needed(a, ["--gpus", "8", "--steps", "20", "--warmup", "5"], env={}) == 0
     assert "--nproc-per-node=8" in seen["cmd"] and "--master-addr=127.0.0.1" in seen["cmd"]
+
+
+def test_rank0_stdout_is_one_json_line_with_gloo(tmp_path):
+    """Two gloo ranks (the driver's N > 1 form on CPU): gloo's C++ connect messages ("[Gloo]
+    Rank r is connected to ...") go to the process's stdout; bench.py routes fd 1 to fd 2
+    around the group's creation, so rank 0's stdout holds only its JSON line."""
+    import json
+    import socket
+    import subprocess
+
+    script = tmp_path / "ranks.py"
+    script.write_text(
+        "import importlib.util, json, os, sys\n"
+        "import torch.distributed as dist\n"
+        f"spec = importlib.util.spec_from_file_location('b', {os.path.join(REPO, 'bench.py')!r})\n"
+        "b = importlib.util.module_from_spec(spec); spec.loader.exec_module(b)\n"
+        "with b.stdout_to_stderr():\n"
+        "    dist.init_process_group('gloo')\n"
+        "    dist.barrier()\n"
+        "dist.barrier()\n"
+        "if dist.get_rank() == 0:\n"
+        "    print(json.dumps({'metric': 'x', 'n': dist.get_world_size()}), flush=True)\n"
+        "dist.destroy_process_group()\n")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), str(script)],
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, out.stdout
+    assert json.loads(lines[0]) == {"metric": "x", "n": 2}
