@@ -31,7 +31,12 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef MOCR_GELU_728
 #define MOCR_GELU_728 0
 #endif
-__device__ __forceinline__ float gelu_erf_fast(float x) {  // gemm.hip gelu_fast (A&S 7.1.26)
+// 2 x GELU(x) = x (1 + erf(x / sqrt 2)) (gemm.hip gelu_fast, A&S 7.1.26, without its factor
+// 0.5): the fused MLP kernels' W2 chunk images hold W2 / 2 (mlp_pack_kernel, pack_img384's
+// W2 image), so GEMM 2 multiplies the same bf16 products -- (2h) (W2 / 2) = h W2 exactly,
+// splits included -- and the outputs are bitwise the unscaled ones, one multiply per
+// hidden value fewer
+__device__ __forceinline__ float gelu2_erf_fast(float x) {
   if constexpr (MOCR_GELU_728) {
     // A&S 7.1.28: erf(z) = 1 - (1 + a1 z + ... + a6 z^6)^-16, |error| <= 3e-7: one
     // reciprocal and no exp (7.1.26 needs both); GELU's absolute error <= 5e-7
@@ -47,7 +52,7 @@ __device__ __forceinline__ float gelu_erf_fast(float x) {  // gemm.hip gelu_fast
     p = p * p;
     p = p * p;
     const float e = 1.0f - __builtin_amdgcn_rcpf(p);
-    return x * 0.5f * (1.0f + copysignf(e, x));
+    return x * (1.0f + copysignf(e, x));
   }
   const float z = fabsf(x) * 0.70710678118654752440f;
   const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
@@ -56,7 +61,7 @@ __device__ __forceinline__ float gelu_erf_fast(float x) {  // gemm.hip gelu_fast
   poly = fmaf(poly, t, -0.284496736f);
   poly = fmaf(poly, t, 0.254829592f);
   const float e = 1.0f - poly * t * __expf(-z * z);
-  return x * 0.5f * (1.0f + copysignf(e, x));
+  return x * (1.0f + copysignf(e, x));
 }
 
 // 8 floats -> bf16 hi / lo planes of one MFMA fragment
@@ -304,8 +309,8 @@ __global__ void __launch_bounds__(64 * NWV) mlp_fused_kernel(MlpParams p) {
           float h[8];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            h[r] = gelu_erf_fast(acc1[2 * kp][tt][r] + bb[r]);
-            h[4 + r] = gelu_erf_fast(acc1[2 * kp + 1][tt][r] + bb[16 + r]);
+            h[r] = gelu2_erf_fast(acc1[2 * kp][tt][r] + bb[r]);
+            h[4 + r] = gelu2_erf_fast(acc1[2 * kp + 1][tt][r] + bb[16 + r]);
           }
           bf16x8 hi, lo;
           pack8(h, hi, lo);
@@ -340,8 +345,8 @@ __global__ void __launch_bounds__(64 * NWV) mlp_fused_kernel(MlpParams p) {
           float h[8];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            h[r] = gelu_erf_fast(acc1[2 * kp][tt][r] + bb[r]);
-            h[4 + r] = gelu_erf_fast(acc1[2 * kp + 1][tt][r] + bb[16 + r]);
+            h[r] = gelu2_erf_fast(acc1[2 * kp][tt][r] + bb[r]);
+            h[4 + r] = gelu2_erf_fast(acc1[2 * kp + 1][tt][r] + bb[16 + r]);
           }
           bf16x8 hi, lo;
           pack8(h, hi, lo);
@@ -445,6 +450,27 @@ __device__ __forceinline__ void dma16(const char* gbase, uint32_t voff, uint32_t
       : "memory");
 }
 
+// Both bf16 halves of v times 0.5 (W2 / 2 for the fused MLPs, gelu2_erf_fast): the exponent
+// minus one, exact for normal values; zeros, and the (never seen) smallest normals and
+// subnormals, through fp32
+__device__ __forceinline__ uint32_t half_bf16x2(uint32_t v) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    uint32_t h = (v >> (16 * i)) & 0xffffu;
+    const uint32_t e = (h >> 7) & 0xffu;
+    if (e > 1u && e < 255u)
+      h -= 0x80u;
+    else if (e <= 1u)
+      h = __float_as_uint(__uint_as_float(h << 16) * 0.5f) >> 16;
+    r |= h << (16 * i);
+  }
+  return r;
+}
+__device__ __forceinline__ uint4 half_bf16x8(uint4 v) {
+  return make_uint4(half_bf16x2(v.x), half_bf16x2(v.y), half_bf16x2(v.z), half_bf16x2(v.w));
+}
+
 // LDS chunk images of the C = 384 kernels, packed once at load: piece `rem` (1 KB) of plane
 // q of chunk jc at (jc * PL + q) * 24 KB + rem * 1024 + 16 * lane holds the 16 B that lane
 // `lane`'s DMA of that piece gathered from the row-major planes, so the kernels' DMA reads
@@ -471,8 +497,9 @@ __global__ void pack_img384_kernel(const char* __restrict__ hi, const char* __re
     src = (size_t)(rem * 16 + (lane >> 2)) * (HID * 2) + jc * 64 + chunk16;
   }
   const char* plane = q ? lo : hi;
-  *reinterpret_cast<uint4*>(out + ((size_t)jc * (lo ? 2 : 1) + q) * PLB + rem * 1024 + 16 * lane) =
-      *reinterpret_cast<const uint4*>(plane + src);
+  const uint4 v = *reinterpret_cast<const uint4*>(plane + src);
+  // W2: W2 / 2 (gelu2_erf_fast)
+  *reinterpret_cast<uint4*>(out + ((size_t)jc * (lo ? 2 : 1) + q) * PLB + rem * 1024 + 16 * lane) = w2 ? half_bf16x8(v) : v;
 }
 
 void pack_img384(const void* hi, const void* lo, int nch, bool w2, void* out, hipStream_t s) {
@@ -687,8 +714,8 @@ __global__ void __launch_bounds__(256) mlp384_kernel(MlpParams p) {
         float h[8];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          h[r] = gelu_erf_fast(acc1[0][tt][r] + bb0[r]);
-          h[4 + r] = gelu_erf_fast(acc1[1][tt][r] + bb1[r]);
+          h[r] = gelu2_erf_fast(acc1[0][tt][r] + bb0[r]);
+          h[4 + r] = gelu2_erf_fast(acc1[1][tt][r] + bb1[r]);
         }
         bf16x8 hi, lo;
         pack8(h, hi, lo);
@@ -969,7 +996,9 @@ __global__ void __launch_bounds__(64) mlp_pack_kernel(MlpParams p, char* __restr
   const int q = P / (I::DMA1 + I::DMA2);
   const int rem = P - q * (I::DMA1 + I::DMA2);
   const uint4 v = mlp_piece_load<C, NC, I::DMA1, I::RC, I::SW1, I::SH1, I::RB, I::SH2>(p, jc, q, rem, lane);
-  *reinterpret_cast<uint4*>(out + (size_t)jc * I::BUF + mlp_piece_dst<I::PL, I::DMA1, I::W1B, I::W2B>(q, rem, lane)) = v;
+  // pieces >= DMA1 are W2's: W2 / 2 (gelu2_erf_fast)
+  *reinterpret_cast<uint4*>(out + (size_t)jc * I::BUF + mlp_piece_dst<I::PL, I::DMA1, I::W1B, I::W2B>(q, rem, lane)) =
+      rem < I::DMA1 ? v : half_bf16x8(v);
 }
 template <int C, int NC>
 void launch_pack_c(const MlpParams& p, void* out, hipStream_t s) {
