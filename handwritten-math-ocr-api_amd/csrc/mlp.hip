@@ -268,7 +268,8 @@ __global__ void __launch_bounds__(64 * NWV) mlp_fused_kernel(MlpParams p) {
     }
     const char* w1s = lds + (NBUF == 2 ? (jc & 1) * BUF : 0);
     const char* w2s = w1s + PL * W1B;
-    // GEMM 1: hidden^T [NC x 16TT] = W1[chunk] . LN(x)^T
+    // GEMM 1: hidden^T [NC x 16TT] = W1[chunk] . LN(x)^T (b1 as the accumulator input, as in
+    // mlp384_kernel, measured slower here: s2.mlp 4.55-4.59 vs 4.41-4.43 ms, profiles/r05/r07c)
     floatx4 acc1[NH][TT];
 #pragma unroll
     for (int ht = 0; ht < NH; ++ht)
@@ -661,11 +662,14 @@ __global__ void __launch_bounds__(256) mlp384_kernel(MlpParams p) {
     // GEMM 1: hidden^T [32 x 32] = W1[chunk, permuted rows] . LN(x)^T.  The fragments of
     // k-step ks + 1 are read while the MFMAs of ks run; the scheduling barriers keep hipcc
     // from hoisting every fragment read of the chunk to the top
+    // b1 as the accumulator input: tile ht, lane group g holds units 8 g + 4 ht .. + 3
     floatx4 acc1[2][TT];
 #pragma unroll
-    for (int ht = 0; ht < 2; ++ht)
+    for (int ht = 0; ht < 2; ++ht) {
+      const floatx4 b4 = *reinterpret_cast<const floatx4*>(b1s + jc * NC + 8 * g + 4 * ht);
 #pragma unroll
-      for (int tt = 0; tt < TT; ++tt) acc1[ht][tt] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int tt = 0; tt < TT; ++tt) acc1[ht][tt] = b4;
+    }
     bf16x8 fa[2][2][PL];
     auto rd1 = [&](int ks, bf16x8(&f)[2][PL]) {
 #pragma unroll
@@ -707,15 +711,13 @@ __global__ void __launch_bounds__(256) mlp384_kernel(MlpParams p) {
     // element r: unit 8 g + 4 ht + r), GEMM 2's B fragment
     bf16x8 hb[TT][PL];
     {
-      const floatx4 bb0 = *reinterpret_cast<const floatx4*>(b1s + jc * NC + 8 * g);
-      const floatx4 bb1 = *reinterpret_cast<const floatx4*>(b1s + jc * NC + 8 * g + 4);
 #pragma unroll
       for (int tt = 0; tt < TT; ++tt) {
         float h[8];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          h[r] = gelu2_erf_fast(acc1[0][tt][r] + bb0[r]);
-          h[4 + r] = gelu2_erf_fast(acc1[1][tt][r] + bb1[r]);
+          h[r] = gelu2_erf_fast(acc1[0][tt][r]);
+          h[4 + r] = gelu2_erf_fast(acc1[1][tt][r]);
         }
         bf16x8 hi, lo;
         pack8(h, hi, lo);
