@@ -129,8 +129,63 @@ __device__ __forceinline__ int mlp_piece_dst(int q, int rem, int lane) {
   return in1 ? q * W1B + sl * 16 : PL * W1B + q * W2B + sl * 16;
 }
 
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ int swz4(int r) { return (0x1320 >> (4 * ((r >> 2) & 3))) & 3; }  // {0,2,3,1}
+
+__device__ __forceinline__ uint32_t lds_u32(const char* p) {
+  return (uint32_t)reinterpret_cast<uintptr_t>((lds_ptr_t)(p));
+}
+// One 1-KB LDS-DMA piece: 16 B per lane from gbase + voff (uniform base, lane offset) to
+// LDS lds + 16 * lane.  Issued by inline asm so that hipcc does not see an LDS write in
+// flight: with __builtin_amdgcn_global_load_lds into a ring indexed at run time it puts a
+// vmcnt(0) before every fragment read.  The kernel waits for its own DMA (counted vmcnt
+// before each barrier); vector loads retire in order, so hipcc's own counts stay safe.
+// M0 is a reserved register (no clobber list entry): the asm saves and restores it.
+__device__ __forceinline__ void dma16(const char* gbase, uint32_t voff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(gbase), "s"(lds)
+      : "memory");
+}
+
+// Both bf16 halves of v times 0.5 (W2 / 2 for the fused MLPs, gelu2_erf_fast): the exponent
+// minus one, exact for normal values; zeros, and the (never seen) smallest normals and
+// subnormals, through fp32
+__device__ __forceinline__ uint32_t half_bf16x2(uint32_t v) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    uint32_t h = (v >> (16 * i)) & 0xffffu;
+    const uint32_t e = (h >> 7) & 0xffu;
+    if (e > 1u && e < 255u)
+      h -= 0x80u;
+    else if (e <= 1u)
+      h = __float_as_uint(__uint_as_float(h << 16) * 0.5f) >> 16;
+    r |= h << (16 * i);
+  }
+  return r;
+}
+__device__ __forceinline__ uint4 half_bf16x8(uint4 v) {
+  return make_uint4(half_bf16x2(v.x), half_bf16x2(v.y), half_bf16x2(v.z), half_bf16x2(v.w));
+}
+
+
+// The stage-1 kernel (C = 96, 4 waves) on three waves per SIMD: its W1 | W2 chunks go to
+// LDS by LDS-DMA (dma16: no staging registers) and its residual rows are loaded in the
+// epilogue, 158 VGPRs and no AGPRs instead of 152 + 68 (two waves per SIMD): s1.mlp 4.73 /
+// 4.78 vs 5.36 / 5.40 ms per 512-image encode, bitwise the same memory (profiles/r05/r07e).
+// A/B builds: -DMOCR_S1_MLP_OCC3=0 -> register staging, two waves per SIMD
+#ifndef MOCR_S1_MLP_OCC3
+#define MOCR_S1_MLP_OCC3 1
+#endif
 template <int C, int TT, int NC, int PASSES, int NWV = 8, int NBUF = 2>
-__global__ void __launch_bounds__(64 * NWV) mlp_fused_kernel(MlpParams p) {
+__global__ void __launch_bounds__(64 * NWV)
+__attribute__((amdgpu_waves_per_eu(C == 96 && NWV == 4 && MOCR_S1_MLP_OCC3 ? 3 : 1, 8)))
+mlp_fused_kernel(MlpParams p) {
+  constexpr bool PRERES = !(C == 96 && NWV == 4 && MOCR_S1_MLP_OCC3);
   constexpr bool X3 = PASSES == 3;
   constexpr int PL = X3 ? 2 : 1;
   constexpr int RC = C / 8;  // 16-B chunks per W1 row
@@ -182,8 +237,22 @@ __global__ void __launch_bounds__(64 * NWV) mlp_fused_kernel(MlpParams p) {
   const char* wpk = static_cast<const char*>(p.wpack);
   auto pdst = [&](int k) { return (k * NWV + wave) * 1024 + lane * 16; };
   auto piece = [&](int jc, int k) { return *reinterpret_cast<const uint4*>(wpk + (size_t)jc * BUF + pdst(k)); };
+  // !PRERES (the 3-wave stage-1 build): the chunks go global -> LDS by LDS-DMA (dma16, no
+  // staging registers), issued at the start of the chunk before the one that reads them
+  constexpr bool DMA = !PRERES;
+  auto issue_chunk = [&](int jc, char* buf) {
+    uint32_t lb = (uint32_t)(16 * lane);
+    asm volatile("" : "+v"(lb));
+#pragma unroll
+    for (int k = 0; k < NST; ++k)
+      dma16(wpk + (size_t)jc * BUF, (uint32_t)((k * NWV + wave) * 1024) + lb,
+            __builtin_amdgcn_readfirstlane(lds_u32(buf) + (k * NWV + wave) * 1024));  // uniform
+  };
   StgList<0, NST> stg;
-  stg.load([&](int k) { return piece(0, k); });
+  if constexpr (DMA)
+    issue_chunk(0, lds);
+  else
+    stg.load([&](int k) { return piece(0, k); });
   for (int i = tid; i < HID; i += 64 * NWV) b1s[i] = p.b1[i];
   for (int i = tid; i < C; i += 64 * NWV) b2s[i] = p.b2[i];
 
@@ -240,7 +309,10 @@ __global__ void __launch_bounds__(64 * NWV) mlp_fused_kernel(MlpParams p) {
       if constexpr (X3) xb[tt][ks][PL - 1] = lo;
     }
   }
-  stg.store([&](int k, const uint4& v) { *reinterpret_cast<uint4*>(lds + pdst(k)) = v; });
+  if constexpr (DMA)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else
+    stg.store([&](int k, const uint4& v) { *reinterpret_cast<uint4*>(lds + pdst(k)) = v; });
   __syncthreads();
 
   floatx4 acc2[NCT][TT];
@@ -254,7 +326,7 @@ __global__ void __launch_bounds__(64 * NWV) mlp_fused_kernel(MlpParams p) {
   floatx4 xres[NCT][TT];
   for (int jc = 0; jc < NCH; ++jc) {
     const bool more = jc + 1 < NCH;
-    if (!more) {
+    if (PRERES && !more) {
 #pragma unroll
       for (int tt = 0; tt < TT; ++tt) {
         const long row = min(row0 + tt * 16 + j16, p.M - 1);
@@ -264,7 +336,10 @@ __global__ void __launch_bounds__(64 * NWV) mlp_fused_kernel(MlpParams p) {
       }
     }
     if (more) {
-      stg.load([&](int k) { return piece(jc + 1, k); });
+      if constexpr (DMA)
+        issue_chunk(jc + 1, lds + (NBUF == 2 ? ((jc + 1) & 1) * BUF : 0));
+      else
+        stg.load([&](int k) { return piece(jc + 1, k); });
     }
     const char* w1s = lds + (NBUF == 2 ? (jc & 1) * BUF : 0);
     const char* w2s = w1s + PL * W1B;
@@ -378,7 +453,9 @@ __global__ void __launch_bounds__(64 * NWV) mlp_fused_kernel(MlpParams p) {
       __builtin_amdgcn_s_setprio(0);
     }
     // the other buffer was last read in chunk jc - 1, before the barrier that ended it
-    if (more) {
+    if (DMA) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk jc + 1 landed (this wave's pieces)
+    } else if (more) {
       if constexpr (NBUF == 1) __syncthreads();  // every wave is done with the one buffer
       char* buf = lds + (NBUF == 2 ? ((jc + 1) & 1) * BUF : 0);
       stg.store([&](int k, const uint4& v) { *reinterpret_cast<uint4*>(buf + pdst(k)) = v; });
@@ -391,6 +468,11 @@ __global__ void __launch_bounds__(64 * NWV) mlp_fused_kernel(MlpParams p) {
   for (int tt = 0; tt < TT; ++tt) {
     const long row = row0 + tt * 16 + j16;
     if (row >= p.M) continue;
+    if constexpr (!PRERES) {  // a row tile's loads all before its first store
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+        xres[ct][tt] = *reinterpret_cast<const floatx4*>(p.X + (size_t)row * C + ct * 16 + 4 * g);
+    }
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct) {
       const int ch = ct * 16 + 4 * g;
@@ -429,49 +511,6 @@ __global__ void __launch_bounds__(64 * NWV) mlp_fused_kernel(MlpParams p) {
 // applied on the DMA's per-lane source address (the LDS side of a DMA is lane-linear).
 // Every DMA source is a uniform base + one lane base + uniform offsets, and every
 // fragment read one lane base + an immediate.
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-
-__device__ __forceinline__ int swz4(int r) { return (0x1320 >> (4 * ((r >> 2) & 3))) & 3; }  // {0,2,3,1}
-
-__device__ __forceinline__ uint32_t lds_u32(const char* p) {
-  return (uint32_t)reinterpret_cast<uintptr_t>((lds_ptr_t)(p));
-}
-// One 1-KB LDS-DMA piece: 16 B per lane from gbase + voff (uniform base, lane offset) to
-// LDS lds + 16 * lane.  Issued by inline asm so that hipcc does not see an LDS write in
-// flight: with __builtin_amdgcn_global_load_lds into a ring indexed at run time it puts a
-// vmcnt(0) before every fragment read.  The kernel waits for its own DMA (counted vmcnt
-// before each barrier); vector loads retire in order, so hipcc's own counts stay safe.
-// M0 is a reserved register (no clobber list entry): the asm saves and restores it.
-__device__ __forceinline__ void dma16(const char* gbase, uint32_t voff, uint32_t lds) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(gbase), "s"(lds)
-      : "memory");
-}
-
-// Both bf16 halves of v times 0.5 (W2 / 2 for the fused MLPs, gelu2_erf_fast): the exponent
-// minus one, exact for normal values; zeros, and the (never seen) smallest normals and
-// subnormals, through fp32
-__device__ __forceinline__ uint32_t half_bf16x2(uint32_t v) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    uint32_t h = (v >> (16 * i)) & 0xffffu;
-    const uint32_t e = (h >> 7) & 0xffu;
-    if (e > 1u && e < 255u)
-      h -= 0x80u;
-    else if (e <= 1u)
-      h = __float_as_uint(__uint_as_float(h << 16) * 0.5f) >> 16;
-    r |= h << (16 * i);
-  }
-  return r;
-}
-__device__ __forceinline__ uint4 half_bf16x8(uint4 v) {
-  return make_uint4(half_bf16x2(v.x), half_bf16x2(v.y), half_bf16x2(v.z), half_bf16x2(v.w));
-}
-
 // LDS chunk images of the C = 384 kernels, packed once at load: piece `rem` (1 KB) of plane
 // q of chunk jc at (jc * PL + q) * 24 KB + rem * 1024 + 16 * lane holds the 16 B that lane
 // `lane`'s DMA of that piece gathered from the row-major planes, so the kernels' DMA reads
