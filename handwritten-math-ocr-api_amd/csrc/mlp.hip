@@ -181,11 +181,20 @@ __device__ __forceinline__ uint4 half_bf16x8(uint4 v) {
 #ifndef MOCR_S1_MLP_OCC3
 #define MOCR_S1_MLP_OCC3 1
 #endif
+// The stage-2 kernel (with MOCR_S2_MLP_NWV = 4) on 4-wave workgroups with one LDS buffer
+// filled by LDS-DMA between two barriers: 148 VGPRs and 53 KB, three workgroups per CU
+// (12 waves) instead of one 8-wave workgroup (229 VGPRs, 102 KB): s2.mlp 4.21 / 4.27 vs
+// 4.53 / 4.61 ms per 512-image encode, bitwise the same memory (profiles/r05/r07h).  With
+// register staging the same geometry measured slower (round 5, r06h: 4.9-5.0 vs 4.5 ms).
+// A/B builds: -DMOCR_S2_MLP_DMA=0 -DMOCR_S2_MLP_NWV=8
+#ifndef MOCR_S2_MLP_DMA
+#define MOCR_S2_MLP_DMA 1
+#endif
 template <int C, int TT, int NC, int PASSES, int NWV = 8, int NBUF = 2>
 __global__ void __launch_bounds__(64 * NWV)
-__attribute__((amdgpu_waves_per_eu(C == 96 && NWV == 4 && MOCR_S1_MLP_OCC3 ? 3 : 1, 8)))
+__attribute__((amdgpu_waves_per_eu((C == 96 && MOCR_S1_MLP_OCC3) || (C == 192 && MOCR_S2_MLP_DMA) ? (NWV == 4 ? 3 : 1) : 1, 8)))
 mlp_fused_kernel(MlpParams p) {
-  constexpr bool PRERES = !(C == 96 && NWV == 4 && MOCR_S1_MLP_OCC3);
+  constexpr bool PRERES = !(NWV == 4 && ((C == 96 && MOCR_S1_MLP_OCC3) || (C == 192 && MOCR_S2_MLP_DMA)));
   constexpr bool X3 = PASSES == 3;
   constexpr int PL = X3 ? 2 : 1;
   constexpr int RC = C / 8;  // 16-B chunks per W1 row
@@ -336,9 +345,9 @@ mlp_fused_kernel(MlpParams p) {
       }
     }
     if (more) {
-      if constexpr (DMA)
-        issue_chunk(jc + 1, lds + (NBUF == 2 ? ((jc + 1) & 1) * BUF : 0));
-      else
+      if constexpr (DMA && NBUF == 2)
+        issue_chunk(jc + 1, lds + ((jc + 1) & 1) * BUF);
+      else if constexpr (!DMA)
         stg.load([&](int k) { return piece(jc + 1, k); });
     }
     const char* w1s = lds + (NBUF == 2 ? (jc & 1) * BUF : 0);
@@ -453,7 +462,14 @@ mlp_fused_kernel(MlpParams p) {
       __builtin_amdgcn_s_setprio(0);
     }
     // the other buffer was last read in chunk jc - 1, before the barrier that ended it
-    if (DMA) {
+    if (DMA && NBUF == 1) {
+      // one buffer: every wave is done with chunk jc before chunk jc + 1 lands in its place
+      if (more) {
+        __syncthreads();
+        issue_chunk(jc + 1, lds);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (DMA) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk jc + 1 landed (this wave's pieces)
     } else if (more) {
       if constexpr (NBUF == 1) __syncthreads();  // every wave is done with the one buffer
@@ -1068,9 +1084,10 @@ void launch_mlp_c(const MlpParams& p, hipStream_t s) {
 #ifndef MOCR_S1_MLP_NWV
 #define MOCR_S1_MLP_NWV 4
 #endif
-// stage 2 (A/B builds: -DMOCR_S2_MLP_NWV=4: 4-wave workgroups of 64 rows, one LDS buffer)
+// stage 2: 4-wave workgroups of 64 rows, one LDS buffer filled by LDS-DMA (MOCR_S2_MLP_DMA;
+// A/B builds: -DMOCR_S2_MLP_NWV=8 -DMOCR_S2_MLP_DMA=0 -> 8 waves, two register-staged buffers)
 #ifndef MOCR_S2_MLP_NWV
-#define MOCR_S2_MLP_NWV 8
+#define MOCR_S2_MLP_NWV 4
 #endif
 constexpr int kS1MlpNC = MOCR_S1_MLP_NWV == 4 ? 32 : 64;
 
