@@ -570,14 +570,22 @@ void pack_img384(const void* hi, const void* lo, int nch, bool w2, void* out, hi
 #ifndef MOCR_MLP384_PROBE
 #define MOCR_MLP384_PROBE 0
 #endif
-template <int PASSES>
-__global__ void __launch_bounds__(256) mlp384_kernel(MlpParams p) {
-  constexpr int C = 384, HID = 4 * C, NC = 32, NCH = HID / NC, KS1 = C / 32, NCT = C / 16, TT = 2;
+// A/B builds: -DMOCR_MLP384_NW=8 -> two waves per SIMD of 16 rows (250 VGPRs, no AGPRs):
+// s3.mlp 10.40 / 10.37 vs 10.47 / 10.26 ms, bitwise the same (profiles/r05/r07i): no gain
+#ifndef MOCR_MLP384_NW
+#define MOCR_MLP384_NW 4
+#endif
+// NW waves of 128 / NW rows each (TT = 8 / NW row tiles): 4 (one wave per SIMD, 512
+// registers) or 8 (two per SIMD, 16 rows each: the same rows per weight stream, twice the
+// LDS fragment reads per MFMA, the other wave's MFMAs beside each wave's reads)
+template <int PASSES, int NW = 4>
+__global__ void __launch_bounds__(64 * NW) mlp384_kernel(MlpParams p) {
+  constexpr int C = 384, HID = 4 * C, NC = 32, NCH = HID / NC, KS1 = C / 32, NCT = C / 16, TT = 8 / NW;
   constexpr bool X3 = PASSES == 3;
   constexpr int PL = X3 ? 2 : 1;
-  constexpr int PLB = NC * C * 2;             // bytes of one plane of a W1 or W2 chunk (24 KB)
-  constexpr int NPW = PL * (PLB / 1024) / 4;  // 1-KB DMA pieces per wave per matrix and chunk
-  static_assert(NPW * 4 * 1024 == PL * PLB && NPW <= KS1 && 2 * NPW <= NCT, "DMA split");
+  constexpr int PLB = NC * C * 2;              // bytes of one plane of a W1 or W2 chunk (24 KB)
+  constexpr int NPW = PL * (PLB / 1024) / NW;  // 1-KB DMA pieces per wave per matrix and chunk
+  static_assert(NPW * NW * 1024 == PL * PLB && NPW <= KS1 && 2 * NPW <= NCT, "DMA split");
   // a ring of three half-chunk slots (W1(0), W2(0), W1(1), ... in turn): two in flight
   // while the MFMAs read the third
   constexpr int SLOT = PL * PLB;
@@ -613,7 +621,7 @@ __global__ void __launch_bounds__(256) mlp384_kernel(MlpParams p) {
     for (int i = i0; i < i0 + n; ++i) {
       // piece i of this wave: plane q = i / (NPW / PL) (compile-time), piece 4 (i % ..) + wave
       const int q = i / (NPW / PL);
-      const int rem = (i - q * (NPW / PL)) * 4 + wave;
+      const int rem = (i - q * (NPW / PL)) * NW + wave;
       const int jr = MOCR_MLP384_PROBE >= 4 ? 0 : jc;
       const uint32_t off = (uint32_t)(jr * SLOT + q * PLB + rem * 1024) + lb;
       dma16(w1g, off, lds_u32(w1s) + q * PLB + rem * 1024);
@@ -626,7 +634,7 @@ __global__ void __launch_bounds__(256) mlp384_kernel(MlpParams p) {
 #pragma unroll
     for (int i = i0; i < i0 + n; ++i) {
       const int q = i / (NPW / PL);
-      const int pp = (i - q * (NPW / PL)) * 4 + wave;
+      const int pp = (i - q * (NPW / PL)) * NW + wave;
       const int jr = MOCR_MLP384_PROBE >= 4 ? 0 : jc;
       const uint32_t off = (uint32_t)(jr * SLOT + q * PLB + pp * 1024) + lb;
       dma16(w2g, off, lds_u32(w2s) + q * PLB + pp * 1024);
@@ -637,8 +645,8 @@ __global__ void __launch_bounds__(256) mlp384_kernel(MlpParams p) {
   auto slot = [&](int hc) { return ring + (hc % 3) * SLOT; };
   issue_w1(0, slot(0), 0, NPW);
   issue_w2(0, slot(1), 0, NPW);
-  for (int i = tid; i < HID; i += 256) b1s[i] = p.b1[i];
-  for (int i = tid; i < C; i += 256) b2s[i] = p.b2[i];
+  for (int i = tid; i < HID; i += 64 * NW) b1s[i] = p.b1[i];
+  for (int i = tid; i < C; i += 64 * NW) b2s[i] = p.b2[i];
 
   // LayerNorm(norm2) of this wave's 2 x 16 rows into GEMM 1's B fragments (lane (g, j):
   // row j of tile tt, channels 32 ks + 8 g .. + 7)
@@ -1156,9 +1164,9 @@ void launch_mlp_fused(const MlpParams& p, hipStream_t s) {
     case 384: {
       const unsigned grid = (unsigned)((p.M + 127) / 128);
       if (p.w1lo)
-        mlp384_kernel<3><<<grid, 256, 0, s>>>(p);
+        mlp384_kernel<3, MOCR_MLP384_NW><<<grid, 64 * MOCR_MLP384_NW, 0, s>>>(p);
       else
-        mlp384_kernel<1><<<grid, 256, 0, s>>>(p);
+        mlp384_kernel<1, MOCR_MLP384_NW><<<grid, 64 * MOCR_MLP384_NW, 0, s>>>(p);
       break;
     }
     default: throw std::runtime_error("mlp: fused MLP built for C = 96, 192, 384");
