@@ -165,6 +165,9 @@ void launch_ln_group(const float* X, const float* g, const float* b, const RowOu
 // Conv2d(1, 96, 4, 4) + LayerNorm(96): 16 lanes per token, 6 channels per lane whose
 // 6x16 weights stay in registers over a grid-stride loop of tokens; the token's 4x4
 // patch is 4 float4 loads (shared by the 16 lanes); LayerNorm over the 16 lanes.
+#ifndef MOCR_STEM_LDS_STORE  // A/B: 1 -> whole 16-B stores through LDS, 5% slower (profiles/r05/r07j/)
+#define MOCR_STEM_LDS_STORE 0
+#endif
 __global__ void __launch_bounds__(256) stem16_kernel(const float* __restrict__ img, const float* __restrict__ w,
                                                      const float* __restrict__ bias, const float* __restrict__ g,
                                                      const float* __restrict__ beta, float* __restrict__ X, long ntok,
@@ -172,6 +175,7 @@ __global__ void __launch_bounds__(256) stem16_kernel(const float* __restrict__ i
   const int lane = threadIdx.x & 63;
   const int gi = lane & 15;
   const int c0 = gi * 6;
+  __shared__ __attribute__((aligned(16))) float stem_out[MOCR_STEM_LDS_STORE ? 4 * 384 : 4];
   float wr[6][16], br[6], gr[6], be[6];
 #pragma unroll
   for (int c = 0; c < 6; ++c) {
@@ -221,13 +225,35 @@ __global__ void __launch_bounds__(256) stem16_kernel(const float* __restrict__ i
     }
     q = row_sum<16>(q);
     const float rstd = 1.0f / sqrtf(q / 96.f + 1e-5f);
-    float* dst = X + (size_t)tok * 96 + c0;
     float o[6];
 #pragma unroll
     for (int c = 0; c < 6; ++c) o[c] = (v[c] - mean) * rstd * gr[c] + be[c];
-    *reinterpret_cast<float2*>(dst) = make_float2(o[0], o[1]);
-    *reinterpret_cast<float2*>(dst + 2) = make_float2(o[2], o[3]);
-    *reinterpret_cast<float2*>(dst + 4) = make_float2(o[4], o[5]);
+    if constexpr (MOCR_STEM_LDS_STORE) {
+      // the wave's 4 consecutive tokens (1536 contiguous bytes of X) through its LDS slice,
+      // then out as whole 16-B lanes: 1 KB + 512 B per store instruction instead of three
+      // 8-B stores per lane 24 B apart
+      float* ws = stem_out + (threadIdx.x >> 6) * 384;
+      const int tw = (threadIdx.x >> 4) & 3;  // token within the wave
+#pragma unroll
+      for (int e = 0; e < 3; ++e)
+        *reinterpret_cast<float2*>(ws + tw * 96 + c0 + 2 * e) = make_float2(o[2 * e], o[2 * e + 1]);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const long tok0 = tok - tw;  // the wave's first token
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int f = lane + 64 * k;  // float4 index in the wave's 96
+        if (f < 96 && tok0 + f / 24 < ntok)
+          *reinterpret_cast<floatx4*>(X + (size_t)tok0 * 96 + 4 * f) = *reinterpret_cast<const floatx4*>(ws + 4 * f);
+      }
+      __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next iteration
+    } else {
+      float* dst = X + (size_t)tok * 96 + c0;
+      *reinterpret_cast<float2*>(dst) = make_float2(o[0], o[1]);
+      *reinterpret_cast<float2*>(dst + 2) = make_float2(o[2], o[3]);
+      *reinterpret_cast<float2*>(dst + 4) = make_float2(o[4], o[5]);
+    }
   }
 }
 
@@ -673,9 +699,13 @@ void launch_stem(const float* img, const float* w, const float* b, const float* 
   const int Hs = H / 4, Ws = W / 4;
   if (W % 4 != 0) throw std::runtime_error("stem: image width must be a multiple of 4");
   const long ntok = (long)B * Hs * Ws;
-  // 1024 workgroups (9 tokens per wave at B = 64, 384²): 121 -> 111 us against 4096, whose
-  // waves paid the weight prologue for 2-3 tokens each (profiles/r02/ab_stem_grid.log)
-  const unsigned blocks = (unsigned)std::min<long>((ntok + 15) / 16, 1024);
+  // One resident round: 768 workgroups = 256 CUs x 3 waves per SIMD (150 VGPRs). 4096 paid
+  // the weight prologue for 2-3 tokens per wave (profiles/r02/ab_stem_grid.log); 1024 left a
+  // quarter-full second round: 829 -> 748 us per 512-image encode (profiles/r05/r07k/)
+#ifndef MOCR_STEM_BLOCKS
+#define MOCR_STEM_BLOCKS 768
+#endif
+  const unsigned blocks = (unsigned)std::min<long>((ntok + 15) / 16, MOCR_STEM_BLOCKS);
   stem16_kernel<<<blocks, 256, 0, s>>>(img, w, b, ln_w, ln_b, X, ntok, H, W, Hs, Ws);
   MOCR_HIP_CHECK(hipGetLastError());
 }
