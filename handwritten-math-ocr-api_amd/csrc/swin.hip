@@ -165,9 +165,6 @@ void launch_ln_group(const float* X, const float* g, const float* b, const RowOu
 // Conv2d(1, 96, 4, 4) + LayerNorm(96): 16 lanes per token, 6 channels per lane whose
 // 6x16 weights stay in registers over a grid-stride loop of tokens; the token's 4x4
 // patch is 4 float4 loads (shared by the 16 lanes); LayerNorm over the 16 lanes.
-#ifndef MOCR_STEM_LDS_STORE  // A/B: 1 -> whole 16-B stores through LDS, 5% slower (profiles/r05/r07j/)
-#define MOCR_STEM_LDS_STORE 0
-#endif
 __global__ void __launch_bounds__(256) stem16_kernel(const float* __restrict__ img, const float* __restrict__ w,
                                                      const float* __restrict__ bias, const float* __restrict__ g,
                                                      const float* __restrict__ beta, float* __restrict__ X, long ntok,
@@ -175,7 +172,6 @@ __global__ void __launch_bounds__(256) stem16_kernel(const float* __restrict__ i
   const int lane = threadIdx.x & 63;
   const int gi = lane & 15;
   const int c0 = gi * 6;
-  __shared__ __attribute__((aligned(16))) float stem_out[MOCR_STEM_LDS_STORE ? 4 * 384 : 4];
   float wr[6][16], br[6], gr[6], be[6];
 #pragma unroll
   for (int c = 0; c < 6; ++c) {
@@ -228,32 +224,105 @@ __global__ void __launch_bounds__(256) stem16_kernel(const float* __restrict__ i
     float o[6];
 #pragma unroll
     for (int c = 0; c < 6; ++c) o[c] = (v[c] - mean) * rstd * gr[c] + be[c];
-    if constexpr (MOCR_STEM_LDS_STORE) {
-      // the wave's 4 consecutive tokens (1536 contiguous bytes of X) through its LDS slice,
-      // then out as whole 16-B lanes: 1 KB + 512 B per store instruction instead of three
-      // 8-B stores per lane 24 B apart
-      float* ws = stem_out + (threadIdx.x >> 6) * 384;
-      const int tw = (threadIdx.x >> 4) & 3;  // token within the wave
+    float* dst = X + (size_t)tok * 96 + c0;
+    *reinterpret_cast<float2*>(dst) = make_float2(o[0], o[1]);
+    *reinterpret_cast<float2*>(dst + 2) = make_float2(o[2], o[3]);
+    *reinterpret_cast<float2*>(dst + 4) = make_float2(o[4], o[5]);
+  }
+}
+
+// The same per-token arithmetic with the patch loads spread over the wave: each lane loads
+// one float4 (a patch row) of 16 consecutive tokens, one sweep ahead, and the four 16-lane
+// groups read their tokens' patches back from the wave's 1 KB LDS slice. The 4-float4-per-
+// lane form keeps one wave's 4 patches (256 B) in flight per HBM round trip; this one 16
+// patches plus the next sweep's 16.
+__global__ void __launch_bounds__(256) stem16w_kernel(const float* __restrict__ img, const float* __restrict__ w,
+                                                      const float* __restrict__ bias, const float* __restrict__ g,
+                                                      const float* __restrict__ beta, float* __restrict__ X, long ntok,
+                                                      int H, int W, int Hs, int Ws) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int gi = lane & 15;
+  const int grp = lane >> 4;
+  const int c0 = gi * 6;
+  __shared__ floatx4 patch[4][64];  // per wave: 16 tokens x 4 patch rows
+  float wr[6][16], br[6], gr[6], be[6];
 #pragma unroll
-      for (int e = 0; e < 3; ++e)
-        *reinterpret_cast<float2*>(ws + tw * 96 + c0 + 2 * e) = make_float2(o[2 * e], o[2 * e + 1]);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const long tok0 = tok - tw;  // the wave's first token
+  for (int c = 0; c < 6; ++c) {
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int f = lane + 64 * k;  // float4 index in the wave's 96
-        if (f < 96 && tok0 + f / 24 < ntok)
-          *reinterpret_cast<floatx4*>(X + (size_t)tok0 * 96 + 4 * f) = *reinterpret_cast<const floatx4*>(ws + 4 * f);
-      }
-      __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next iteration
-    } else {
-      float* dst = X + (size_t)tok * 96 + c0;
-      *reinterpret_cast<float2*>(dst) = make_float2(o[0], o[1]);
-      *reinterpret_cast<float2*>(dst + 2) = make_float2(o[2], o[3]);
-      *reinterpret_cast<float2*>(dst + 4) = make_float2(o[4], o[5]);
+    for (int k4 = 0; k4 < 4; ++k4) {
+      const floatx4 t = *reinterpret_cast<const floatx4*>(w + (c0 + c) * 16 + 4 * k4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wr[c][4 * k4 + e] = t[e];
     }
+    br[c] = bias[c0 + c];
+    gr[c] = g[c0 + c];
+    be[c] = beta[c0 + c];
+  }
+  const long hw = (long)Hs * Ws;
+  auto load_row = [&](long t0) -> floatx4 {  // row lane % 4 of token t0 + lane / 4 (clamped)
+    long tok = t0 + (lane >> 2);
+    tok = tok < ntok ? tok : ntok - 1;
+    const int b = (int)(tok / hw);
+    const int rem = (int)(tok - (long)b * hw);
+    const int y = rem / Ws;
+    const int x = rem - y * Ws;
+    return *reinterpret_cast<const floatx4*>(img + ((size_t)b * H + 4 * y + (lane & 3)) * W + 4 * x);
+  };
+  const long sweep = (long)gridDim.x * 64;  // tokens per sweep of all waves
+  long t0 = ((long)blockIdx.x * 4 + wave) * 16;
+  if (t0 >= ntok) return;  // wave-uniform
+  floatx4 next = load_row(t0);
+  for (; t0 < ntok; t0 += sweep) {
+    patch[wave][lane] = next;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (t0 + sweep < ntok) next = load_row(t0 + sweep);
+#pragma unroll 1
+    for (int j = 0; j < 4; ++j) {
+      const int tw = 4 * j + grp;  // token within the wave's 16
+      const long tok = t0 + tw;
+      float px[16];
+#pragma unroll
+      for (int ky = 0; ky < 4; ++ky) {
+        const floatx4 t = patch[wave][4 * tw + ky];
+        px[4 * ky] = t[0];
+        px[4 * ky + 1] = t[1];
+        px[4 * ky + 2] = t[2];
+        px[4 * ky + 3] = t[3];
+      }
+      float v[6];
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc = fmaf(wr[c][k], px[k], acc);
+        v[c] = acc + br[c];
+        s += v[c];
+      }
+      s = row_sum<16>(s);
+      const float mean = s / 96.f;
+      float q = 0.f;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const float d = v[c] - mean;
+        q += d * d;
+      }
+      q = row_sum<16>(q);
+      const float rstd = 1.0f / sqrtf(q / 96.f + 1e-5f);
+      float o[6];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) o[c] = (v[c] - mean) * rstd * gr[c] + be[c];
+      if (tok < ntok) {
+        float* dst = X + (size_t)tok * 96 + c0;
+        *reinterpret_cast<float2*>(dst) = make_float2(o[0], o[1]);
+        *reinterpret_cast<float2*>(dst + 2) = make_float2(o[2], o[3]);
+        *reinterpret_cast<float2*>(dst + 4) = make_float2(o[4], o[5]);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next sweep
   }
 }
 
@@ -705,8 +774,16 @@ void launch_stem(const float* img, const float* w, const float* b, const float* 
 #ifndef MOCR_STEM_BLOCKS
 #define MOCR_STEM_BLOCKS 768
 #endif
-  const unsigned blocks = (unsigned)std::min<long>((ntok + 15) / 16, MOCR_STEM_BLOCKS);
-  stem16_kernel<<<blocks, 256, 0, s>>>(img, w, b, ln_w, ln_b, X, ntok, H, W, Hs, Ws);
+#ifndef MOCR_STEM_WAVE16  // A/B builds: 1 -> stem16w_kernel
+#define MOCR_STEM_WAVE16 0
+#endif
+  if (MOCR_STEM_WAVE16) {
+    const unsigned blocks = (unsigned)std::min<long>((ntok + 63) / 64, MOCR_STEM_BLOCKS);
+    stem16w_kernel<<<blocks, 256, 0, s>>>(img, w, b, ln_w, ln_b, X, ntok, H, W, Hs, Ws);
+  } else {
+    const unsigned blocks = (unsigned)std::min<long>((ntok + 15) / 16, MOCR_STEM_BLOCKS);
+    stem16_kernel<<<blocks, 256, 0, s>>>(img, w, b, ln_w, ln_b, X, ntok, H, W, Hs, Ws);
+  }
   MOCR_HIP_CHECK(hipGetLastError());
 }
 
