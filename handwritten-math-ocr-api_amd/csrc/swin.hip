@@ -236,6 +236,7 @@ __global__ void __launch_bounds__(256) stem16_kernel(const float* __restrict__ i
 // groups read their tokens' patches back from the wave's 1 KB LDS slice. The 4-float4-per-
 // lane form keeps one wave's 4 patches (256 B) in flight per HBM round trip; this one 16
 // patches plus the next sweep's 16.
+template <int DEPTH>
 __global__ void __launch_bounds__(256) stem16w_kernel(const float* __restrict__ img, const float* __restrict__ w,
                                                       const float* __restrict__ bias, const float* __restrict__ g,
                                                       const float* __restrict__ beta, float* __restrict__ X, long ntok,
@@ -272,13 +273,18 @@ __global__ void __launch_bounds__(256) stem16w_kernel(const float* __restrict__ 
   const long sweep = (long)gridDim.x * 64;  // tokens per sweep of all waves
   long t0 = ((long)blockIdx.x * 4 + wave) * 16;
   if (t0 >= ntok) return;  // wave-uniform
-  floatx4 next = load_row(t0);
+  floatx4 next[DEPTH];  // the patch rows of the next DEPTH sweeps
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d)
+    if (d == 0 || t0 + d * sweep < ntok) next[d] = load_row(t0 + d * sweep);
   for (; t0 < ntok; t0 += sweep) {
-    patch[wave][lane] = next;
+    patch[wave][lane] = next[0];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (t0 + sweep < ntok) next = load_row(t0 + sweep);
+#pragma unroll
+    for (int d = 0; d + 1 < DEPTH; ++d) next[d] = next[d + 1];
+    if (t0 + DEPTH * sweep < ntok) next[DEPTH - 1] = load_row(t0 + DEPTH * sweep);
 #pragma unroll 1
     for (int j = 0; j < 4; ++j) {
       const int tw = 4 * j + grp;  // token within the wave's 16
@@ -774,12 +780,12 @@ void launch_stem(const float* img, const float* w, const float* b, const float* 
 #ifndef MOCR_STEM_BLOCKS
 #define MOCR_STEM_BLOCKS 768
 #endif
-#ifndef MOCR_STEM_WAVE16  // A/B builds: 1 -> stem16w_kernel
-#define MOCR_STEM_WAVE16 0
+#ifndef MOCR_STEM_WAVE16  // stem16w_kernel's prefetch depth in sweeps; 0 -> stem16_kernel
+#define MOCR_STEM_WAVE16 1
 #endif
-  if (MOCR_STEM_WAVE16) {
+  if constexpr (MOCR_STEM_WAVE16 > 0) {
     const unsigned blocks = (unsigned)std::min<long>((ntok + 63) / 64, MOCR_STEM_BLOCKS);
-    stem16w_kernel<<<blocks, 256, 0, s>>>(img, w, b, ln_w, ln_b, X, ntok, H, W, Hs, Ws);
+    stem16w_kernel<MOCR_STEM_WAVE16><<<blocks, 256, 0, s>>>(img, w, b, ln_w, ln_b, X, ntok, H, W, Hs, Ws);
   } else {
     const unsigned blocks = (unsigned)std::min<long>((ntok + 15) / 16, MOCR_STEM_BLOCKS);
     stem16_kernel<<<blocks, 256, 0, s>>>(img, w, b, ln_w, ln_b, X, ntok, H, W, Hs, Ws);
