@@ -716,6 +716,21 @@ __global__ void split_bf16_kernel(const float* __restrict__ x, RowOut out, size_
   for (; i < n; i += stride) store_val(out, i, x[i]);
 }
 
+// the same split, 4 values per lane per iteration (float4 in, two 8-B stores out)
+__global__ void split4_bf16_kernel(const floatx4* __restrict__ x, uint2* __restrict__ hi, uint2* __restrict__ lo,
+                                   size_t n4) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (; i < n4; i += stride) {
+    const floatx4 v = x[i];
+    uint32_t h0, l0, h1, l1;
+    split2_bf16(v[0], v[1], h0, l0);
+    split2_bf16(v[2], v[3], h1, l1);
+    hi[i] = make_uint2(h0, h1);
+    if (lo) lo[i] = make_uint2(l0, l1);
+  }
+}
+
 // cross K/V fp32 [B * M][512] -> fp24 head-major planes [B][2][8][M][32], 4 columns per thread
 __global__ void split_kv_fp24_kernel(const float* __restrict__ kv, uint8_t* __restrict__ kv24, int M, size_t n4) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -874,8 +889,16 @@ void launch_quant_kv_i16(const float* kv, int16_t* q, float* scale, int B, int M
 
 void launch_split_bf16(const float* x, uint16_t* hi, uint16_t* lo, size_t n, hipStream_t s) {
   if (n == 0) return;
-  const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 65536);
-  split_bf16_kernel<<<blocks, 256, 0, s>>>(x, RowOut{nullptr, hi, lo}, n);
+  const auto al = [](const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
+  if (n % 4 == 0 && al(x, 16) && al(hi, 8) && al(lo, 8)) {  // split(memory): 158 -> ~90 us per 512 images
+    const size_t n4 = n / 4;
+    const unsigned blocks = (unsigned)std::min<size_t>((n4 + 255) / 256, 65536);
+    split4_bf16_kernel<<<blocks, 256, 0, s>>>(reinterpret_cast<const floatx4*>(x), reinterpret_cast<uint2*>(hi),
+                                              reinterpret_cast<uint2*>(lo), n4);
+  } else {
+    const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 65536);
+    split_bf16_kernel<<<blocks, 256, 0, s>>>(x, RowOut{nullptr, hi, lo}, n);
+  }
   MOCR_HIP_CHECK(hipGetLastError());
 }
 
