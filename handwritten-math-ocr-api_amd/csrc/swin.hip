@@ -236,6 +236,9 @@ __global__ void __launch_bounds__(256) stem16_kernel(const float* __restrict__ i
 // groups read their tokens' patches back from the wave's 1 KB LDS slice. The 4-float4-per-
 // lane form keeps one wave's 4 patches (256 B) in flight per HBM round trip; this one 16
 // patches plus the next sweep's 16.
+#ifndef MOCR_STEM_LDS_OUT  // 1: X leaves through an LDS slice as whole 16-B lanes (596 -> 457 us
+#define MOCR_STEM_LDS_OUT 1  // per 512 images, profiles/r05/r07q/); 0: three 8-B stores per lane
+#endif
 template <int DEPTH>
 __global__ void __launch_bounds__(256) stem16w_kernel(const float* __restrict__ img, const float* __restrict__ w,
                                                       const float* __restrict__ bias, const float* __restrict__ g,
@@ -247,6 +250,7 @@ __global__ void __launch_bounds__(256) stem16w_kernel(const float* __restrict__ 
   const int grp = lane >> 4;
   const int c0 = gi * 6;
   __shared__ floatx4 patch[4][64];  // per wave: 16 tokens x 4 patch rows
+  __shared__ __attribute__((aligned(16))) float xout[4][MOCR_STEM_LDS_OUT ? 16 * 96 : 4];  // per wave: 16 tokens of X
   float wr[6][16], br[6], gr[6], be[6];
 #pragma unroll
   for (int c = 0; c < 6; ++c) {
@@ -321,14 +325,29 @@ __global__ void __launch_bounds__(256) stem16w_kernel(const float* __restrict__ 
       float o[6];
 #pragma unroll
       for (int c = 0; c < 6; ++c) o[c] = (v[c] - mean) * rstd * gr[c] + be[c];
-      if (tok < ntok) {
+      if constexpr (MOCR_STEM_LDS_OUT) {
+        float* os = xout[wave] + tw * 96 + c0;
+#pragma unroll
+        for (int e = 0; e < 3; ++e) *reinterpret_cast<float2*>(os + 2 * e) = make_float2(o[2 * e], o[2 * e + 1]);
+      } else if (tok < ntok) {
         float* dst = X + (size_t)tok * 96 + c0;
         *reinterpret_cast<float2*>(dst) = make_float2(o[0], o[1]);
         *reinterpret_cast<float2*>(dst + 2) = make_float2(o[2], o[3]);
         *reinterpret_cast<float2*>(dst + 4) = make_float2(o[4], o[5]);
       }
     }
-    __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next sweep
+    if constexpr (MOCR_STEM_LDS_OUT) {  // the 16 tokens' 6 KB of X as whole 1 KB store instructions
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 2
+      for (int k = 0; k < 6; ++k) {
+        const int f = lane + 64 * k;  // float4 index among the 16 tokens' 384
+        if (t0 + f / 24 < ntok)
+          *reinterpret_cast<floatx4*>(X + (size_t)t0 * 96 + 4 * f) = *reinterpret_cast<const floatx4*>(xout[wave] + 4 * f);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the slices are rewritten by the next sweep
   }
 }
 
