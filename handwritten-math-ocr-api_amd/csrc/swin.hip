@@ -55,6 +55,9 @@ struct LnGeom {
   WinGeom win;
 };
 
+#ifndef MOCR_LN_LDS_OUT  // 1: bf16 planes through LDS as whole 16-B lanes (merge2 / merge3 norms
+#define MOCR_LN_LDS_OUT 1  // 408 / 276 -> 304 / 180 us per 512 images, profiles/r05/r07r/)
+#endif
 template <int LPR, int F, int MODE>
 __global__ void __launch_bounds__(256) ln_group_kernel(const float* __restrict__ X, const float* __restrict__ g,
                                                        const float* __restrict__ b, RowOut out, LnGeom geo) {
@@ -130,6 +133,37 @@ __global__ void __launch_bounds__(256) ln_group_kernel(const float* __restrict__
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[e + k] = (v[e + k] - mean) * rstd * gg[k] + bb[k];
     }
+  }
+  if (MOCR_LN_LDS_OUT && !out.f32 && out.hi) {
+    // the wave's RPW rows are 64 F contiguous outputs: each plane goes through the wave's
+    // LDS slice and leaves as whole 16-B lanes (8 bf16), not F / 4 8-B stores per lane
+    __shared__ __attribute__((aligned(16))) uint32_t st[4][32 * F];
+    uint32_t* ws = st[threadIdx.x >> 6];
+    const long row0 = row - lane / LPR;  // the wave's first row
+    const size_t base = (size_t)row0 * geo.C;
+    uint32_t hp[F / 2], lp[F / 2];
+#pragma unroll
+    for (int e = 0; e < F; e += 2) split2_bf16(v[e], v[e + 1], hp[e / 2], lp[e / 2]);
+#pragma unroll
+    for (int plane = 0; plane < 2; ++plane) {
+      uint16_t* dst = plane ? out.lo : out.hi;
+      if (!dst) break;  // wave-uniform
+#pragma unroll
+      for (int e = 0; e < F / 2; e += 2)
+        *reinterpret_cast<uint2*>(ws + lane * (F / 2) + e) = plane ? make_uint2(lp[e], lp[e + 1]) : make_uint2(hp[e], hp[e + 1]);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int k = 0; k < (8 * F + 63) / 64; ++k) {
+        const int f = lane + 64 * k;  // 16-B chunk of the wave's 128 F bytes
+        if ((8 * F) % 64 == 0 || f < 8 * F)
+          if (row0 + (8 * f) / geo.C < geo.rows)
+            *reinterpret_cast<uint4*>(dst + base + 8 * f) = *reinterpret_cast<const uint4*>(ws + 4 * f);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    return;
   }
   if (!live) return;
   const size_t off = (size_t)row * geo.C + c0;
