@@ -456,6 +456,9 @@ __global__ void __launch_bounds__(2 * C * WPB) __attribute__((amdgpu_waves_per_e
 // C of the no-proj kernels: attention of one head (K, V^T, Q^T fragments as B leaves
 // them) per 16-query tile; O goes to the ATT planes [window token row, C] at channels
 // ch0 + {4g.., 16+4g..} (tok0 = the window's first row)
+#ifndef MOCR_ATT_STORE16  // A/B builds: 1 -> the ATT planes as 16-B stores (lane pairs trade
+#define MOCR_ATT_STORE16 0   // halves): 12 B of scratch at C = 384, s3.attn 1 % slower (r05/r07t)
+#endif
 template <bool X3, int C>
 __device__ __forceinline__ void attend_to_planes(const bf16x8 (&kf)[4][2], const bf16x8 (&vf)[2][2][2],
                                                  const bf16x8 (&qf4)[4][2], const float* tb, int j16, int g,
@@ -518,7 +521,28 @@ __device__ __forceinline__ void attend_to_planes(const bf16x8 (&kf)[4][2], const
     }
     // ATT planes [row, C]: query token 16qt + j16 -> row orow[qt] (-1: not written),
     // channels 32h + {4g.., 16+4g..}
-    if (orow[qt] >= 0) {
+    if (MOCR_ATT_STORE16 && orow[qt] >= 0) {
+      // lanes g and g ^ 1 (16 apart, the same query row) trade halves so that each holds 8
+      // consecutive channels: even g the dt = 0 run 4g .. 4g + 7, odd g the dt = 1 run
+      // 16 + 4(g - 1) .. 16 + 4g + 3; one 16-B store per plane instead of two 8-B ones
+      const bool odd = g & 1;
+      const size_t off = (size_t)orow[qt] * C + ch0 + (odd ? 16 + 4 * (g - 1) : 4 * g);
+#pragma unroll
+      for (int plane = 0; plane < (X3 ? 2 : 1); ++plane) {  // one plane at a time (registers)
+        uint32_t v[2][2], t;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            if (plane) split2_bf16(x[4 * dt + 2 * e], x[4 * dt + 2 * e + 1], t, v[dt][e]);
+            else split2_bf16(x[4 * dt + 2 * e], x[4 * dt + 2 * e + 1], v[dt][e], t);
+          }
+        const uint32_t r0 = __shfl_xor(odd ? v[0][0] : v[1][0], 16);
+        const uint32_t r1 = __shfl_xor(odd ? v[0][1] : v[1][1], 16);
+        *reinterpret_cast<uint4*>((plane ? att_lo : att_hi) + off) =
+            odd ? make_uint4(r0, r1, v[1][0], v[1][1]) : make_uint4(v[0][0], v[0][1], r0, r1);
+      }
+    } else if (orow[qt] >= 0) {
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
         const size_t off = (size_t)orow[qt] * C + ch0 + 16 * dt + 4 * g;
