@@ -550,7 +550,9 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
 // Cross-attention on int16 K/V with 16-B loads: 4 lanes per key row (8 columns each), 16
 // key rows per wave instruction (dec_foldattn_kernel: 8 lanes of 8-B loads, 8 rows). The
 // same arithmetic per score and per output column, summed in a different order.
-#ifndef MOCR_XATTN_LPR4  // A/B builds: 1 -> dec_xattn16_kernel for the int16 cross-attention
+// Measured slower: the decode step 440 -> 469 us at 512 rows (2 or 3 waves), the extra
+// cross-lane sums and registers outweigh the halved load count (profiles/r05/r07u/).
+#ifndef MOCR_XATTN_LPR4  // A/B builds: 1 / 2 -> dec_xattn16_kernel on 2 / 3 waves
 #define MOCR_XATTN_LPR4 0
 #endif
 __device__ __forceinline__ void ld_stream_i16x8(const int16_t* base, size_t e, floatx4& a, floatx4& b) {
