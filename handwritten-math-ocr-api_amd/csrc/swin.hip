@@ -584,6 +584,9 @@ __device__ __forceinline__ floatx4 mfma3(const abf16x8& ah, const abf16x8& al, c
 // token's k / v then take the bias (selected, bitwise the old path's value) in the
 // windows that have one (a wave-uniform ballot).  The launcher splits the batch into
 // image chunks of < 2 GiB of QKV rows.
+#ifndef MOCR_WATT_STORE16  // 1: the O planes as 16-B stores, lane pairs trading halves (s4.wattn
+#define MOCR_WATT_STORE16 1  // 614 -> 558 us per 512 images, profiles/r05/r07x/); 0: 8-B stores
+#endif
 template <int PASSES>
 __global__ void __launch_bounds__(256) window_attention_mfma_kernel(const float* __restrict__ QKV,
                                                                     const float* __restrict__ table, RowOut out,
@@ -743,11 +746,16 @@ __global__ void __launch_bounds__(256) window_attention_mfma_kernel(const float*
       for (int j = 0; j < 8; ++j) x[j] = st[2 * s + (j >> 2)][j & 3] * rs;
       split8(x, ph[s], pl[s]);
     }
+    floatx4 od[2];
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) {
       floatx4 o = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 2; ++s) o = mfma3<PASSES>(vh[dt][s], vl[dt][s], ph[s], pl[s], o);
+      if (MOCR_WATT_STORE16 && !out.f32) {
+        od[dt] = o;
+        continue;
+      }
       if (qr >= 0) {
         const size_t off = (size_t)qr * C + h * kHeadDim + 16 * dt + 4 * g;
         if (out.f32) *reinterpret_cast<floatx4*>(out.f32 + off) = o;
@@ -758,6 +766,28 @@ __global__ void __launch_bounds__(256) window_attention_mfma_kernel(const float*
           *reinterpret_cast<uint2*>(out.hi + off) = make_uint2(h0, h1);
           if (out.lo) *reinterpret_cast<uint2*>(out.lo + off) = make_uint2(l0, l1);
         }
+      }
+    }
+    if (MOCR_WATT_STORE16 && !out.f32 && out.hi && qr >= 0) {
+      // lanes g and g ^ 1 (16 apart, the same query row) trade halves: 8 consecutive
+      // channels per lane, one 16-B store per plane (attend_to_planes in wattn.hip)
+      const bool odd = g & 1;
+      const size_t off = (size_t)qr * C + h * kHeadDim + (odd ? 16 + 4 * (g - 1) : 4 * g);
+#pragma unroll
+      for (int plane = 0; plane < 2; ++plane) {
+        uint16_t* dst = plane ? out.lo : out.hi;
+        if (!dst) break;
+        uint32_t v[2][2], t;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            if (plane) split2_bf16(od[dt][2 * e], od[dt][2 * e + 1], t, v[dt][e]);
+            else split2_bf16(od[dt][2 * e], od[dt][2 * e + 1], v[dt][e], t);
+          }
+        const uint32_t r0 = __shfl_xor(odd ? v[0][0] : v[1][0], 16);
+        const uint32_t r1 = __shfl_xor(odd ? v[0][1] : v[1][1], 16);
+        *reinterpret_cast<uint4*>(dst + off) = odd ? make_uint4(r0, r1, v[1][0], v[1][1]) : make_uint4(v[0][0], v[0][1], r0, r1);
       }
     }
   }
