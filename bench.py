@@ -384,10 +384,14 @@ def main():
     def run(n, pool=pool):
         lat = []
         for ids, dt in pool.imap(step, range(n)):
+            # the all-gather of the token streams, in call order: RCCL on device memory, or the
+            # host group when ranks share a device; through the pad-and-trim gather any shard
+            # split takes (every rank's call holds BG rows here, so it is one plain gather)
             if grp:
-                grp.gather_ids(ids)  # RCCL all-gather of the token streams, in call order
+                pkg.parallel.gather_shards(ids, world * BG, world, rank, grp.gather_ids)
             elif world > 1:
-                pkg.parallel.gather_ids_host(ids.cpu(), world)
+                pkg.parallel.gather_shards(ids.cpu(), world * BG, world, rank,
+                                           lambda t: pkg.parallel.gather_ids_host(t, world))
             lat.append(dt)
         return lat
 

@@ -9,6 +9,7 @@ Routes and payloads follow the reference:
 Differences, all on the compute side:
 
 - ``/predict/batch`` decodes every valid image of the request as ONE batch on the GPU. The reference loops image by image. Per-image results are unchanged; see ``im2latex.predict_batch``. If the batched call fails, each image is retried alone, so only the images that fail on their own are reported ``success: false`` (the reference's per-image error isolation, :562-570).
+- ``/predict`` requests that arrive together are decoded together: a micro-batcher (``app/batcher.py``) opens a 2 ms window at the first request and sends every request inside it, up to the engine's ``max_batch``, to the engine as one call. Each request gets the result its image gets alone (the reference calls the model once per request, :486).
 - Engine calls run in a worker thread. The reference calls the model synchronously on the event loop (:486). ctypes releases the GIL, and a lock serialises calls on the one engine.
 - ``/metrics`` adds the engine's images/s and a histogram of engine-call latencies to the reference's keys.
 
@@ -19,6 +20,7 @@ reference does when its limiter is missing.
 """
 from __future__ import annotations
 
+import asyncio
 import base64
 import io
 import os
@@ -35,6 +37,7 @@ from starlette.concurrency import run_in_threadpool
 from .. import im2latex
 from ..config import config
 from ..preprocess import preprocess_image
+from .batcher import MicroBatcher
 
 API_TITLE = "Handwritten Math Formula Recognition API"
 API_VERSION = "1.0.0"
@@ -122,7 +125,11 @@ class State:
     """Model state of one server process (the reference keeps module globals)."""
 
     def __init__(self, engine=None, vocab=None, idx2char=None, predictor: Optional[Callable] = None,
-                 device: str = "cuda:0", model_dir: Optional[str] = None, checkpoint: str = "model.pth"):
+                 device: str = "cuda:0", model_dir: Optional[str] = None, checkpoint: str = "model.pth",
+                 batch_window_ms: Optional[float] = None, max_batch: Optional[int] = None):
+        """``batch_window_ms`` / ``max_batch``: the /predict micro-batcher's window (default
+        ``MOCR_BATCH_WINDOW_MS`` or 2 ms) and largest batch (default the engine's
+        ``max_batch``, or ``config.max_batch_images`` with an injected predictor)."""
         self.engine = engine
         self.vocab = vocab
         self.idx2char = idx2char
@@ -138,6 +145,26 @@ class State:
         self.images_done = 0
         self.gpu_seconds = 0.0
         self.latency_counts = [0] * (len(LATENCY_BUCKETS_MS) + 1)
+        if batch_window_ms is None:
+            batch_window_ms = float(os.environ.get("MOCR_BATCH_WINDOW_MS", "2"))
+        if max_batch is None:
+            max_batch = engine.max_batch if engine is not None else config.max_batch_images
+        self.batch_window_ms = batch_window_ms
+        self.max_batch = max_batch
+        self._batcher: Optional[MicroBatcher] = None
+        self._batcher_lock = threading.Lock()
+
+    @property
+    def batcher(self) -> MicroBatcher:
+        """The /predict micro-batcher, started on first use."""
+        with self._batcher_lock:
+            if self._batcher is None:
+                self._batcher = MicroBatcher(self.run, self.max_batch, self.batch_window_ms * 1e-3)
+            return self._batcher
+
+    def close(self):
+        if self._batcher is not None:
+            self._batcher.close()
 
     @property
     def loaded(self):
@@ -213,7 +240,8 @@ def create_app(state: Optional[State] = None, model_dir: Optional[str] = None) -
             raise HTTPException(status_code=413, detail=f"File too large. Maximum size: {config.max_file_size} bytes")
         image = preprocess_image(_decode_image(data))
         try:
-            (formula, confidence), = await run_in_threadpool(st.run, image)
+            # joins the requests arriving within the batching window: one engine call for all
+            formula, confidence = await asyncio.wrap_future(st.batcher.submit(image))
         except Exception as e:  # noqa: BLE001
             raise HTTPException(status_code=500, detail=f"Prediction failed: {e}") from e
         st.predictions += 1
@@ -322,9 +350,14 @@ def create_app(state: Optional[State] = None, model_dir: Optional[str] = None) -
             for b, n in zip(list(LATENCY_BUCKETS_MS) + ["+Inf"], st.latency_counts):
                 cum += n
                 buckets[f"le_{b}"] = cum
+            b = st._batcher
             out["engine"] = {"images_processed": st.images_done, "engine_seconds": st.gpu_seconds,
                              "images_per_engine_second": st.images_done / st.gpu_seconds if st.gpu_seconds else None,
-                             "call_latency_ms_histogram": buckets}
+                             "call_latency_ms_histogram": buckets,
+                             "predict_microbatch": {"window_ms": st.batch_window_ms, "max_batch": st.max_batch,
+                                                    "engine_calls": b.calls if b else 0,
+                                                    "mean_batch": (sum(b.batch_sizes) / len(b.batch_sizes))
+                                                    if b and b.batch_sizes else None}}
         return out
 
     return app

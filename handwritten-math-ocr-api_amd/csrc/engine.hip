@@ -238,7 +238,7 @@ void check_config(const mocr_config& c) {
                       MOCR_VARIANT_S4_FUSED_ATTN | MOCR_VARIANT_WINDOW_ROWS | MOCR_VARIANT_DEC_NARROW |
                       MOCR_VARIANT_LOGITS_F32 | MOCR_VARIANT_S3_LARGE_BATCH | MOCR_VARIANT_KV_F32 |
                       MOCR_VARIANT_CROSS_KV_F24 | MOCR_VARIANT_UNFUSED_LN_GEMM | MOCR_VARIANT_SELF_KV_F24 |
-                      MOCR_VARIANT_BEAM_UNFOLDED)) == 0,
+                      MOCR_VARIANT_BEAM_UNFOLDED | MOCR_VARIANT_UNFUSED_S3_TAIL)) == 0,
       "variant: unknown MOCR_VARIANT_* flag");
   req(c.sos_id >= 0 && c.sos_id < c.vocab && c.eos_id >= 0 && c.eos_id < c.vocab, "special ids");
 }
@@ -1054,6 +1054,10 @@ struct mocr_engine {
           mp.w1lo = dwl ? dwl + w.fc1w : nullptr;
           mp.w2 = dwh + w.fc2w;
           mp.w2lo = dwl ? dwl + w.fc2w : nullptr;
+          if (C == 384) {  // W_proj's chunk images for the block tail kernel (s3_tail_fused)
+            mp.wproj = dwh + w.projw;
+            mp.wproj_lo = dwl ? dwl + w.projw : nullptr;
+          }
           launch_mlp_pack(mp, mlppack[bi], stream);
         }
         // lngemm384's W_qkv image: stage 3's norm1 + qkv runs on it only when its fused
@@ -1226,6 +1230,13 @@ struct mocr_engine {
   // B = 256: 989 vs 1298 us per block for ln2 + fc1 + fc2; at B = 64 its 288 workgroups
   // take two rounds, 476 vs 334 us, profiles/r03/mlp384_*.log)
   bool s3_large(int B) const { return B >= 128 || (cfg.variant & MOCR_VARIANT_S3_LARGE_BATCH); }
+  // stage 3's block tail at >= 128 images: the attention output
+  // projection + residual inside the fused MLP kernel (mlp.hip mlp384_kernel PROJ), which
+  // takes O from the fused attention's ATT planes in X's row order
+  bool s3_tail_fused(int C, int B) const {
+    return C == 384 && bf16_mode() && noproj_fused(C, B) && s3_large(B) && mlp_fused() && mlp_fused_supported(C) &&
+           !(cfg.variant & MOCR_VARIANT_UNFUSED_S3_TAIL);
+  }
   int attn_passes() const {
     return cfg.precision == MOCR_PRECISION_FP32 ? 0 : (cfg.precision == MOCR_PRECISION_BF16X3 ? 3 : 1);
   }
@@ -1365,8 +1376,9 @@ struct mocr_engine {
           ap.wg = wg;
           timed(attn_n[s], 6.0 * rows * C * C + 4.0 * rows * kWinTok * C, 4.0 * rows * C + (dwl ? 4.0 : 2.0) * 3.0 * C * C +
                 (dwl ? 4.0 : 2.0) * rows * C, [&] { launch_swin_attn_noproj(ap, stream); });
-          gemm(proj_n[s], opATT, wop(w.projw), W(w.projb), X, nullptr, nullptr, (int)rows, C, C, EPI_RESADD, nullptr,
-               rows);
+          if (!s3_tail_fused(C, B))
+            gemm(proj_n[s], opATT, wop(w.projw), W(w.projb), X, nullptr, nullptr, (int)rows, C, C, EPI_RESADD, nullptr,
+                 rows);
         } else if (b16 && !(cfg.variant & MOCR_VARIANT_WINDOW_ROWS)) {
           // the image's tokens only (stage 4 at 384²: 144 of 196 window slots per image):
           // norm1 and qkv in X's row order, the attention kernel maps window slots to pixels
@@ -1420,7 +1432,16 @@ struct mocr_engine {
           mp.w2lo = dwl ? dwl + w.fc2w : nullptr;
           mp.b2 = W(w.fc2b);
           mp.wpack = bi < (int)mlppack.size() ? mlppack[bi] : nullptr;
-          timed(mlp_n[s], 16.0 * rows * C * C, 8.0 * rows * C + (dwl ? 4.0 : 2.0) * 8.0 * C * C,
+          const bool tail = s3_tail_fused(C, B);
+          if (tail) {  // proj + residual in front of norm2 (the block tail, "s3.tail")
+            mp.att_hi = ATTh;
+            mp.att_lo = dwl ? ATTl : nullptr;
+            mp.wproj = dwh + w.projw;
+            mp.wproj_lo = dwl ? dwl + w.projw : nullptr;
+            mp.bproj = W(w.projb);
+          }
+          timed(tail ? "s3.tail" : mlp_n[s], (tail ? 18.0 : 16.0) * rows * C * C,
+                (tail ? 12.0 + (dwl ? 4.0 : 2.0) : 8.0) * rows * C + (dwl ? 4.0 : 2.0) * (tail ? 9.0 : 8.0) * C * C,
                 [&] { launch_mlp_fused(mp, stream); });
         } else {
           timed(ln2_n[s], 0, 8.0 * rows * C,

@@ -124,6 +124,13 @@ struct MlpParams {
   const void *w2, *w2lo;    // [C, 4C]
   const float* b2;          // [C]
   const void* wpack;        // W1 | W2 as the kernel's LDS chunk images (launch_mlp_pack)
+  // C = 384 only: the block's attention output projection fused in front (mlp384_kernel
+  // PROJ): X = x_mid + mlp(norm2(x_mid)), x_mid = X + O W_proj^T + b_proj.  att_hi / att_lo:
+  // O as bf16 planes [M, C] in X's row order; wproj / wproj_lo: W_proj's planes, packed
+  // by launch_mlp_pack after W2 (null: no proj, or no proj images packed)
+  const uint16_t *att_hi, *att_lo;
+  const void *wproj, *wproj_lo;
+  const float* bproj;
 };
 bool mlp_fused_supported(int C);
 void launch_mlp_fused(const MlpParams& p, hipStream_t s);

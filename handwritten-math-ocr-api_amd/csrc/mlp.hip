@@ -133,6 +133,15 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 __device__ __forceinline__ int swz4(int r) { return (0x1320 >> (4 * ((r >> 2) & 3))) & 3; }  // {0,2,3,1}
 
+// GEMM 2's output channels are permuted (the W2 image's row i holds W2 row perm384(i), and
+// b2 likewise), so that lane group g of output tiles 2 ks, 2 ks + 1 holds channels 32 ks +
+// 8 g .. + 7: the B-fragment layout of the LayerNorm's input.  For GEMM 2 alone that only
+// moves which lane computes a channel (bitwise the same outputs); with PROJ it lets the
+// proj GEMM's accumulators be the LayerNorm's input in place.
+__device__ __forceinline__ int perm384(int i) {
+  return 32 * (i >> 5) + 8 * ((i >> 2) & 3) + 4 * ((i >> 4) & 1) + (i & 3);
+}
+
 __device__ __forceinline__ uint32_t lds_u32(const char* p) {
   return (uint32_t)reinterpret_cast<uintptr_t>((lds_ptr_t)(p));
 }
@@ -533,9 +542,11 @@ mlp_fused_kernel(MlpParams p) {
 // 1 KB of contiguous memory per piece instead of 16 rows x 64 B.
 //  - W1 image (lngemm384's W, mlp384's W1; [N, 384], 32-unit chunks): piece rem = 2 ks + h,
 //    row jc*32 + 4 h + 8 g + (lane / 4) % 4, bytes ks*64 + 16 ((lane & 3) ^ f(lane / 4));
-//  - W2 image (mlp384's W2 [384, 1536]): piece pp, row 16 pp + lane / 4, bytes jc*64 +
-//    16 ((lane & 3) ^ f(lane / 4)).
-__global__ void pack_img384_kernel(const char* __restrict__ hi, const char* __restrict__ lo, int nch, int w2,
+//  - W2 image (mlp384's W2 [384, 1536]), mode 1: piece pp, row perm384(16 pp + lane / 4),
+//    bytes jc*64 + 16 ((lane & 3) ^ f(lane / 4)), halved (gelu2_erf_fast);
+//  - W_proj image (mlp384<PROJ>'s W_proj [384, 384]), mode 2: as W2's over 384 input
+//    channels, not halved.
+__global__ void pack_img384_kernel(const char* __restrict__ hi, const char* __restrict__ lo, int nch, int mode,
                                    char* __restrict__ out) {
   constexpr int C = 384, HID = 4 * C, PLB = 32 * C * 2;
   const int lane = threadIdx.x & 63;
@@ -546,52 +557,56 @@ __global__ void pack_img384_kernel(const char* __restrict__ hi, const char* __re
   const int g = lane >> 4;
   const int chunk16 = ((lane & 3) ^ swz4(lane >> 2)) << 4;
   size_t src;
-  if (!w2) {
+  if (mode == 0) {
     const int ks = rem >> 1, h = rem & 1;
     src = (size_t)(jc * 32 + 4 * h + 8 * g + ((lane >> 2) & 3)) * (C * 2) + ks * 64 + chunk16;
   } else {
-    src = (size_t)(rem * 16 + (lane >> 2)) * (HID * 2) + jc * 64 + chunk16;
+    src = (size_t)perm384(rem * 16 + (lane >> 2)) * ((mode == 1 ? HID : C) * 2) + jc * 64 + chunk16;
   }
   const char* plane = q ? lo : hi;
   const uint4 v = *reinterpret_cast<const uint4*>(plane + src);
   // W2: W2 / 2 (gelu2_erf_fast)
-  *reinterpret_cast<uint4*>(out + ((size_t)jc * (lo ? 2 : 1) + q) * PLB + rem * 1024 + 16 * lane) = w2 ? half_bf16x8(v) : v;
+  *reinterpret_cast<uint4*>(out + ((size_t)jc * (lo ? 2 : 1) + q) * PLB + rem * 1024 + 16 * lane) =
+      mode == 1 ? half_bf16x8(v) : v;
 }
 
-void pack_img384(const void* hi, const void* lo, int nch, bool w2, void* out, hipStream_t s) {
+void pack_img384(const void* hi, const void* lo, int nch, int mode, void* out, hipStream_t s) {
   pack_img384_kernel<<<nch * (lo ? 2 : 1) * 24, 64, 0, s>>>(static_cast<const char*>(hi), static_cast<const char*>(lo),
-                                                            nch, w2 ? 1 : 0, static_cast<char*>(out));
+                                                            nch, mode, static_cast<char*>(out));
   MOCR_HIP_CHECK(hipGetLastError());
 }
 
-// timing probes (tools/build_variant.sh DIR -DMOCR_MLP384_PROBE=N; wrong results):
-// 1 no weight DMA, 2 no MFMA, 3 no vmcnt wait before the barriers, 4 every chunk's DMA
-// reads chunk 0 (an L2-resident 96 KB), 5 = 4 + 2
-#ifndef MOCR_MLP384_PROBE
-#define MOCR_MLP384_PROBE 0
-#endif
-// A/B builds: -DMOCR_MLP384_NW=8 -> two waves per SIMD of 16 rows (250 VGPRs, no AGPRs):
-// s3.mlp 10.40 / 10.37 vs 10.47 / 10.26 ms, bitwise the same (profiles/r05/r07i): no gain
-#ifndef MOCR_MLP384_NW
-#define MOCR_MLP384_NW 4
-#endif
+
 // NW waves of 128 / NW rows each (TT = 8 / NW row tiles): 4 (one wave per SIMD, 512
-// registers) or 8 (two per SIMD, 16 rows each: the same rows per weight stream, twice the
-// LDS fragment reads per MFMA, the other wave's MFMAs beside each wave's reads)
-template <int PASSES, int NW = 4>
+// registers); an 8-wave form (two per SIMD of 16 rows) measured no faster (profiles/r05/r07i).
+//
+// PROJ (the stage-3 block tail as one row-tile kernel): the block's
+// attention output projection, residual add and norm2 run here too --
+//   x_mid = X + (O W_proj^T + b_proj),  X = x_mid + mlp(norm2(x_mid))
+// (torchvision SwinTransformerBlock: x = x + attn(norm1(x)); x = x + mlp(norm2(x))).  O
+// (the attention kernel's bf16 hi / lo planes in X's row order) is loaded as the B
+// fragments GEMM 1 later takes from the LayerNorm; W_proj streams through the same LDS ring
+// as 12 chunk images of 32 input channels (W2's image geometry, rows permuted the same way)
+// ahead of W1(0); the proj accumulators land in GEMM 2's accumulators, so x_mid is formed
+// in the LayerNorm's lane layout and GEMM 2 then accumulates on top of it.  X is read once
+// and written once; the separate proj GEMM's write and the MLP's two re-reads of X are gone.
+template <int PASSES, bool PROJ, int NW = 4>
 __global__ void __launch_bounds__(64 * NW) mlp384_kernel(MlpParams p) {
   constexpr int C = 384, HID = 4 * C, NC = 32, NCH = HID / NC, KS1 = C / 32, NCT = C / 16, TT = 8 / NW;
+  constexpr int NPJ = C / NC;  // proj chunk images (32 input channels each)
   constexpr bool X3 = PASSES == 3;
   constexpr int PL = X3 ? 2 : 1;
-  constexpr int PLB = NC * C * 2;              // bytes of one plane of a W1 or W2 chunk (24 KB)
+  constexpr int PLB = NC * C * 2;              // bytes of one plane of a W1, W2 or W_proj chunk (24 KB)
   constexpr int NPW = PL * (PLB / 1024) / NW;  // 1-KB DMA pieces per wave per matrix and chunk
   static_assert(NPW * NW * 1024 == PL * PLB && NPW <= KS1 && 2 * NPW <= NCT, "DMA split");
-  // a ring of three half-chunk slots (W1(0), W2(0), W1(1), ... in turn): two in flight
-  // while the MFMAs read the third
+  static_assert(NPJ % 3 == 0, "the proj chunks leave the ring's slot numbering of the MLP chunks unchanged");
+  // a ring of three half-chunk slots (W1(0), W2(0), W1(1), ... in turn; PROJ: W_proj's 12
+  // chunks first): two in flight while the MFMAs read the third
   constexpr int SLOT = PL * PLB;
   __shared__ __attribute__((aligned(16))) char ring[3 * SLOT];
   __shared__ __attribute__((aligned(16))) float b1s[HID];
-  __shared__ __attribute__((aligned(16))) float b2s[C];
+  __shared__ __attribute__((aligned(16))) float b2s[C];                 // b2[perm384(i)]
+  __shared__ __attribute__((aligned(16))) float bps[PROJ ? C : 1];      // b_proj[perm384(i)]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -599,22 +614,24 @@ __global__ void __launch_bounds__(64 * NW) mlp384_kernel(MlpParams p) {
   const int j16 = lane & 15;
   const int g = lane >> 4;
   const long row0 = (long)blockIdx.x * 128 + wave * 16 * TT;
-  // the packed chunk images (pack_img384): W1's chunks, then W2's
+  // the packed chunk images (pack_img384): W1's chunks, then W2's, then (PROJ) W_proj's
   const char* w1g = static_cast<const char*>(p.wpack);
   const char* w2g = w1g + (size_t)NCH * SLOT;
+  const char* wpg = w2g + (size_t)NCH * SLOT;
 
   // W1 piece (plane q, k-step ks, half h): LDS rows u = 16 h + lane / 4 of block ks, slot
   // lane % 4; row u is hidden unit pi(u) = 8 g + 4 h + (lane / 4) % 4 of the chunk, and
   // slot s holds the channel chunk s ^ f(g) of k-step ks.
-  // W2 piece (plane q, pp): LDS rows r = 16 pp + lane / 4 (channels), slot s holds the
-  // chunk's hidden units 8 (s ^ f(g)) .. + 7.
-  const uint32_t lb1 = (uint32_t)(16 * lane), lb2 = lb1;
+  // W2 / W_proj piece (plane q, pp): LDS rows r = 16 pp + lane / 4 (output channels
+  // perm384(r)), slot s holds the chunk's k 8 (s ^ f(g)) .. + 7.
+  // Every image has one piece geometry: piece i of this wave's share of chunk jc at
+  // (jc * SLOT + q * PLB + rem * 1024) + 16 lane, only the image base differs.
+  const uint32_t lb1 = (uint32_t)(16 * lane);
   // (the empty asm makes the lane base look new in every call: hipcc would otherwise hoist
   // the 24 per-piece 64-bit addresses out of the chunk loop and spill them)
-  // pieces [i0, i0 + n) of this wave's share (the chunk loop issues one piece per MFMA step:
+  // pieces [i0, i0 + n) of this wave's share (the chunk loops issue one piece per MFMA step:
   // a burst of 12 DMA instructions stalls the wave's issue, and its MFMAs with it)
-  auto issue_w1 = [&](int jc, char* w1s, int i0, int n) {
-    if (MOCR_MLP384_PROBE == 1) return;
+  auto issue = [&](const char* base, int jc, char* dst, int i0, int n) __attribute__((always_inline)) {
     uint32_t lb = lb1;
     asm volatile("" : "+v"(lb));
 #pragma unroll
@@ -622,48 +639,135 @@ __global__ void __launch_bounds__(64 * NW) mlp384_kernel(MlpParams p) {
       // piece i of this wave: plane q = i / (NPW / PL) (compile-time), piece 4 (i % ..) + wave
       const int q = i / (NPW / PL);
       const int rem = (i - q * (NPW / PL)) * NW + wave;
-      const int jr = MOCR_MLP384_PROBE >= 4 ? 0 : jc;
-      const uint32_t off = (uint32_t)(jr * SLOT + q * PLB + rem * 1024) + lb;
-      dma16(w1g, off, lds_u32(w1s) + q * PLB + rem * 1024);
+      const uint32_t off = (uint32_t)(jc * SLOT + q * PLB + rem * 1024) + lb;
+      dma16(base, off, lds_u32(dst) + q * PLB + rem * 1024);
     }
   };
-  auto issue_w2 = [&](int jc, char* w2s, int i0, int n) {
-    if (MOCR_MLP384_PROBE == 1) return;
-    uint32_t lb = lb2;
-    asm volatile("" : "+v"(lb));
+
+  // ring item hc (the MLP's half chunks; PROJ's 12 proj chunks are items -12 .. -1):
+  // W1(hc / 2) if even, W2(hc / 2) if odd, in slot hc % 3
+  auto slot = [&](int hc) { return ring + ((hc + 3 * NPJ) % 3) * SLOT; };
+  // fragment reads: row v = 16 t + j16 of a 64-B-row image, chunk g at g ^ f(j16 / 4)
+  const int fo = j16 * 64 + ((g ^ swz4(j16)) << 4);
+
+  bf16x8 xb[TT][KS1][PL];  // GEMM 1's B fragments (PROJ: first O's, the proj GEMM's)
+  floatx4 acc2[NCT][TT];
 #pragma unroll
-    for (int i = i0; i < i0 + n; ++i) {
-      const int q = i / (NPW / PL);
-      const int pp = (i - q * (NPW / PL)) * NW + wave;
-      const int jr = MOCR_MLP384_PROBE >= 4 ? 0 : jc;
-      const uint32_t off = (uint32_t)(jr * SLOT + q * PLB + pp * 1024) + lb;
-      dma16(w2g, off, lds_u32(w2s) + q * PLB + pp * 1024);
+  for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt) acc2[ct][tt] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  if constexpr (PROJ) {
+    // O rows as B fragments (lane (g, j): row j of tile tt, channels 32 kc + 8 g .. + 7),
+    // loaded before the first DMA so that the ring's vmcnt waits cover them
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt) {
+      const long row = min(row0 + tt * 16 + j16, p.M - 1);
+#pragma unroll
+      for (int kc = 0; kc < KS1; ++kc)
+#pragma unroll
+        for (int q = 0; q < PL; ++q)
+          xb[tt][kc][q] = *reinterpret_cast<const bf16x8*>((q ? p.att_lo : p.att_hi) + (size_t)row * C + 32 * kc + 8 * g);
+    }
+    issue(wpg, 0, slot(-NPJ), 0, NPW);
+    issue(wpg, 1, slot(-NPJ + 1), 0, NPW);
+  } else {
+    issue(w1g, 0, slot(0), 0, NPW);
+    issue(w2g, 0, slot(1), 0, NPW);
+  }
+  for (int i = tid; i < HID; i += 64 * NW) b1s[i] = p.b1[i];
+  for (int i = tid; i < C; i += 64 * NW) b2s[i] = p.b2[perm384(i)];
+  if constexpr (PROJ)
+    for (int i = tid; i < C; i += 64 * NW) bps[i] = p.bproj[perm384(i)];
+
+  // GEMM 2's loop body over one W2-geometry chunk in slot `ws`: out^T [384 x 32] +=
+  // W[:, chunk] . B^T, one channel tile per step, the next tile's fragments read ahead,
+  // one DMA piece of the item two ahead issued every other step
+  auto gemm2 = [&](const char* ws, auto bf, const char* nbase, int njc, char* ndst, bool nxt)
+                   __attribute__((always_inline)) {
+    bf16x8 fb[2][PL];
+    auto rd2 = [&](int ct, bf16x8(&f)[PL]) {
+      const int o = fo + ct * 1024;
+      f[0] = *reinterpret_cast<const bf16x8*>(ws + o);
+      if constexpr (X3) f[PL - 1] = *reinterpret_cast<const bf16x8*>(ws + PLB + o);
+    };
+    rd2(0, fb[0]);
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      if (ct + 1 < NCT) rd2(ct + 1, fb[(ct + 1) & 1]);
+      if (nxt && (ct & 1) == 0 && ct / 2 < NPW) issue(nbase, njc, ndst, ct / 2, 1);
+#pragma unroll
+      for (int tt = 0; tt < TT; ++tt) {
+        const bf16x8 ah = fb[ct & 1][0];
+        acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bf(tt, 0), acc2[ct][tt], 0, 0, 0);
+        if constexpr (X3) {
+          const bf16x8 al = fb[ct & 1][PL - 1];
+          acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bf(tt, 1), acc2[ct][tt], 0, 0, 0);
+          acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bf(tt, 0), acc2[ct][tt], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 
-  // half-chunk hc: W1(hc / 2) if even, W2(hc / 2) if odd, into slot hc % 3
-  auto slot = [&](int hc) { return ring + (hc % 3) * SLOT; };
-  issue_w1(0, slot(0), 0, NPW);
-  issue_w2(0, slot(1), 0, NPW);
-  for (int i = tid; i < HID; i += 64 * NW) b1s[i] = p.b1[i];
-  for (int i = tid; i < C; i += 64 * NW) b2s[i] = p.b2[i];
+  if constexpr (PROJ) {
+    // proj^T [384 x 32] = W_proj[perm rows, chunk kc] . O^T, chunk by chunk; item kc + 2 is
+    // W_proj(kc + 2), then W1(0) and W2(0)
+#pragma unroll
+    for (int kc = 0; kc < NPJ; ++kc) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
+      __builtin_amdgcn_s_barrier();
+      const int it2 = kc + 2;  // the item two ahead
+      const char* nb = it2 < NPJ ? wpg : (it2 == NPJ ? w1g : w2g);
+      gemm2(slot(kc - NPJ), [&](int tt, int q) __attribute__((always_inline)) { return xb[tt][kc][q]; }, nb,
+            it2 < NPJ ? it2 : 0, slot(it2 - NPJ), true);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // x_mid = X + (proj + b_proj) in the LayerNorm's lane layout: output tile ct, lane group
+    // g, element r is channel perm384(16 ct + 4 g + r) = 32 (ct / 2) + 8 g + 4 (ct % 2) + r,
+    // so tiles 2 ks, 2 ks + 1 are the channels GEMM 1's B fragment ks takes
+    // (one row tile at a time, its 24 loads in flight together: the scheduling barriers
+    // keep hipcc from hoisting the other tile's loads into this one's registers)
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt) {
+      const long row = min(row0 + tt * 16 + j16, p.M - 1);
+      const float* xr = p.X + (size_t)row * C + 8 * g;
+      floatx4 x4[NCT];
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) x4[ct] = *reinterpret_cast<const floatx4*>(xr + 32 * (ct >> 1) + 4 * (ct & 1));
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+        const floatx4 b4 = *reinterpret_cast<const floatx4*>(bps + 16 * ct + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc2[ct][tt][r] = x4[ct][r] + (acc2[ct][tt][r] + b4[r]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
 
-  // LayerNorm(norm2) of this wave's 2 x 16 rows into GEMM 1's B fragments (lane (g, j):
-  // row j of tile tt, channels 32 ks + 8 g .. + 7)
-  bf16x8 xb[TT][KS1][PL];
+  // LayerNorm(norm2) of this wave's TT x 16 rows into GEMM 1's B fragments (lane (g, j):
+  // row j of tile tt, channels 32 ks + 8 g .. + 7); PROJ: from x_mid in acc2, which then
+  // stays there as GEMM 2's accumulator input (the residual)
 #pragma unroll
   for (int tt = 0; tt < TT; ++tt) {
-    const long row = min(row0 + tt * 16 + j16, p.M - 1);
-    const float* xr = p.X + (size_t)row * C + 8 * g;
     float v[KS1][8];
+    if constexpr (PROJ) {
 #pragma unroll
-    for (int ks = 0; ks < KS1; ++ks) {
-      const floatx4 a = *reinterpret_cast<const floatx4*>(xr + 32 * ks);
-      const floatx4 b = *reinterpret_cast<const floatx4*>(xr + 32 * ks + 4);
+      for (int ks = 0; ks < KS1; ++ks)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[ks][e] = a[e];
-        v[ks][4 + e] = b[e];
+        for (int e = 0; e < 8; ++e) v[ks][e] = acc2[2 * ks + (e >> 2)][tt][e & 3];
+    } else {
+      const long row = min(row0 + tt * 16 + j16, p.M - 1);
+      const float* xr = p.X + (size_t)row * C + 8 * g;
+#pragma unroll
+      for (int ks = 0; ks < KS1; ++ks) {
+        const floatx4 a = *reinterpret_cast<const floatx4*>(xr + 32 * ks);
+        const floatx4 b = *reinterpret_cast<const floatx4*>(xr + 32 * ks + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[ks][e] = a[e];
+          v[ks][4 + e] = b[e];
+        }
       }
     }
     float s = 0.f;
@@ -701,21 +805,13 @@ __global__ void __launch_bounds__(64 * NW) mlp384_kernel(MlpParams p) {
       xb[tt][ks][0] = hi;
       if constexpr (X3) xb[tt][ks][PL - 1] = lo;
     }
+    if constexpr (PROJ) __builtin_amdgcn_sched_barrier(0);  // (registers: one tile's LN at a time)
   }
-
-  // fragment reads: row v = 16 t + j16 of a 64-B-row image, chunk g at g ^ f(j16 / 4)
-  const int fo = j16 * 64 + ((g ^ swz4(j16)) << 4);
-
-  floatx4 acc2[NCT][TT];
-#pragma unroll
-  for (int ct = 0; ct < NCT; ++ct)
-#pragma unroll
-    for (int tt = 0; tt < TT; ++tt) acc2[ct][tt] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   for (int jc = 0; jc < NCH; ++jc) {
     // W1(jc) landed (this wave's pieces; W2(jc)'s may stay in flight), then visible to all;
     // every wave is past GEMM 2 of chunk jc - 1, so its slot takes W1(jc + 1)
-    if (MOCR_MLP384_PROBE != 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
     __builtin_amdgcn_s_barrier();
     const bool nxt = jc + 1 < NCH;
     char* s_w1n = slot(2 * jc + 2);
@@ -744,9 +840,9 @@ __global__ void __launch_bounds__(64 * NW) mlp384_kernel(MlpParams p) {
     };
     rd1(0, fa[0]);
 #pragma unroll
-    for (int ks = 0; ks < (MOCR_MLP384_PROBE == 2 || MOCR_MLP384_PROBE == 5 ? 0 : KS1); ++ks) {
+    for (int ks = 0; ks < KS1; ++ks) {
       if (ks + 1 < KS1) rd1(ks + 1, fa[(ks + 1) & 1]);
-      if (nxt && ks < NPW) issue_w1(jc + 1, s_w1n, ks, 1);
+      if (nxt && ks < NPW) issue(w1g, jc + 1, s_w1n, ks, 1);
 #pragma unroll
       for (int ht = 0; ht < 2; ++ht)
 #pragma unroll
@@ -763,75 +859,52 @@ __global__ void __launch_bounds__(64 * NW) mlp384_kernel(MlpParams p) {
     }
     // W2(jc) landed and visible (W1(jc + 1)'s pieces may stay in flight); every wave is past
     // GEMM 1, so its slot takes W2(jc + 1)
-    if (MOCR_MLP384_PROBE != 3) {
-      if (jc + 1 < NCH)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (jc + 1 < NCH)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     // bias + GELU: lane group g holds hidden units jc*32 + 8 g .. + 7 of row j (tile ht,
     // element r: unit 8 g + 4 ht + r), GEMM 2's B fragment
     bf16x8 hb[TT][PL];
-    {
 #pragma unroll
-      for (int tt = 0; tt < TT; ++tt) {
-        float h[8];
+    for (int tt = 0; tt < TT; ++tt) {
+      float h[8];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          h[r] = gelu2_erf_fast(acc1[0][tt][r]);
-          h[4 + r] = gelu2_erf_fast(acc1[1][tt][r]);
-        }
-        bf16x8 hi, lo;
-        pack8(h, hi, lo);
-        hb[tt][0] = hi;
-        if constexpr (X3) hb[tt][PL - 1] = lo;
+      for (int r = 0; r < 4; ++r) {
+        h[r] = gelu2_erf_fast(acc1[0][tt][r]);
+        h[4 + r] = gelu2_erf_fast(acc1[1][tt][r]);
       }
+      bf16x8 hi, lo;
+      pack8(h, hi, lo);
+      hb[tt][0] = hi;
+      if constexpr (X3) hb[tt][PL - 1] = lo;
     }
-    // GEMM 2: out^T [384 x 32] += W2[:, chunk] . hidden^T, one channel tile per step, the
-    // next tile's fragments read ahead
-    bf16x8 fb[2][PL];
-    auto rd2 = [&](int ct, bf16x8(&f)[PL]) {
-      const int o = fo + ct * 1024;
-      f[0] = *reinterpret_cast<const bf16x8*>(w2s + o);
-      if constexpr (X3) f[PL - 1] = *reinterpret_cast<const bf16x8*>(w2s + PLB + o);
-    };
-    rd2(0, fb[0]);
-#pragma unroll
-    for (int ct = 0; ct < (MOCR_MLP384_PROBE == 2 || MOCR_MLP384_PROBE == 5 ? 0 : NCT); ++ct) {
-      if (ct + 1 < NCT) rd2(ct + 1, fb[(ct + 1) & 1]);
-      if (nxt && (ct & 1) == 0 && ct / 2 < NPW) issue_w2(jc + 1, s_w2n, ct / 2, 1);
-#pragma unroll
-      for (int tt = 0; tt < TT; ++tt) {
-        const bf16x8 ah = fb[ct & 1][0];
-        acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hb[tt][0], acc2[ct][tt], 0, 0, 0);
-        if constexpr (X3) {
-          const bf16x8 al = fb[ct & 1][PL - 1];
-          acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hb[tt][1], acc2[ct][tt], 0, 0, 0);
-          acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, hb[tt][0], acc2[ct][tt], 0, 0, 0);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    }
+    // GEMM 2: out^T [384 x 32] += W2[perm rows, chunk] . hidden^T
+    gemm2(w2s, [&](int tt, int q) __attribute__((always_inline)) { return hb[tt][q]; }, w2g, jc + 1, s_w2n, nxt);
+  }
 
-  // x += out + b2 (4 consecutive channels of one row per lane and tile); a row tile's 24
-  // loads are all issued before its first store (hipcc keeps a load behind an earlier
-  // store to the same buffer: one HBM round trip per tile otherwise)
+  // out = x + mlp + b2 at channels perm384(16 ct + 4 g ..): 4 consecutive channels of one
+  // row per lane and tile.  PROJ: acc2 already holds x_mid + mlp.  Otherwise a row tile's 24
+  // loads are all issued before its first store (hipcc keeps a load behind an earlier store
+  // to the same buffer: one HBM round trip per tile otherwise)
 #pragma unroll
   for (int tt = 0; tt < TT; ++tt) {
     const long row = row0 + tt * 16 + j16;
     if (row >= p.M) continue;
-    float* xr = p.X + (size_t)row * C + 4 * g;
+    float* xr = p.X + (size_t)row * C + 8 * g;
     floatx4 x[NCT];
+    if constexpr (!PROJ) {
 #pragma unroll
-    for (int ct = 0; ct < NCT; ++ct) x[ct] = *reinterpret_cast<const floatx4*>(xr + ct * 16);
+      for (int ct = 0; ct < NCT; ++ct) x[ct] = *reinterpret_cast<const floatx4*>(xr + 32 * (ct >> 1) + 4 * (ct & 1));
+    }
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct) {
-      const int ch = ct * 16 + 4 * g;
+      const floatx4 b4 = *reinterpret_cast<const floatx4*>(b2s + 16 * ct + 4 * g);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) x[ct][r] = x[ct][r] + (acc2[ct][tt][r] + b2s[ch + r]);
-      *reinterpret_cast<floatx4*>(xr + ct * 16) = x[ct];
+      for (int r = 0; r < 4; ++r)
+        x[ct][r] = PROJ ? acc2[ct][tt][r] + b4[r] : x[ct][r] + (acc2[ct][tt][r] + b4[r]);
+      *reinterpret_cast<floatx4*>(xr + 32 * (ct >> 1) + 4 * (ct & 1)) = x[ct];
     }
   }
 }
@@ -1127,12 +1200,13 @@ void launch_lngemm384(const LnGemm384Params& p, hipStream_t s) {
 // hidden chunk NC per C as launch_mlp_fused runs the kernel; C = 384: W1's then W2's images
 size_t mlp_pack_bytes(int C, bool x3) {
   if (C != 96 && C != 192 && C != 384) return 0;
-  return (size_t)(x3 ? 2 : 1) * 4 * C * C * 2 * 2;  // PL x (W1 + W2) bf16
+  // PL x (W1 + W2) bf16, and at C = 384 the W_proj images of the PROJ kernel
+  return (size_t)(x3 ? 2 : 1) * (4 * C * C * 2 + (C == 384 ? C * C : 0)) * 2;
 }
 
 void launch_lngemm384_pack(const void* w, const void* wlo, int N, void* out, hipStream_t s) {
   if (!w || !out || N <= 0 || N % 32 != 0 || N > kLnGemm384MaxN) throw std::runtime_error("lngemm384_pack: N % 32");
-  pack_img384(w, wlo, N / 32, false, out, s);
+  pack_img384(w, wlo, N / 32, 0, out, s);
 }
 
 void launch_mlp_pack(const MlpParams& p, void* out, hipStream_t s) {
@@ -1143,8 +1217,10 @@ void launch_mlp_pack(const MlpParams& p, void* out, hipStream_t s) {
     case 192: launch_pack_c<192, 32>(p, out, s); break;
     case 384: {
       const size_t img = (size_t)4 * 384 * 384 * 2 * (p.w1lo ? 2 : 1);  // W1's 48 chunk images
-      pack_img384(p.w1, p.w1lo, 48, false, out, s);
-      pack_img384(p.w2, p.w2lo, 48, true, static_cast<char*>(out) + img, s);
+      pack_img384(p.w1, p.w1lo, 48, 0, out, s);
+      pack_img384(p.w2, p.w2lo, 48, 1, static_cast<char*>(out) + img, s);
+      // mlp384<PROJ>'s W_proj: 12 chunk images after W2's (mlp_pack_bytes counts them)
+      if (p.wproj) pack_img384(p.wproj, p.wproj_lo, 12, 2, static_cast<char*>(out) + 2 * img, s);
       break;
     }
     default: throw std::runtime_error("mlp_pack: built for C = 96, 192, 384");
@@ -1163,10 +1239,16 @@ void launch_mlp_fused(const MlpParams& p, hipStream_t s) {
     case 192: launch_mlp_c<192, 1, 32, MOCR_S2_MLP_NWV, MOCR_S2_MLP_NWV == 4 ? 1 : 2>(p, s); break;
     case 384: {
       const unsigned grid = (unsigned)((p.M + 127) / 128);
-      if (p.w1lo)
-        mlp384_kernel<3, MOCR_MLP384_NW><<<grid, 64 * MOCR_MLP384_NW, 0, s>>>(p);
-      else
-        mlp384_kernel<1, MOCR_MLP384_NW><<<grid, 64 * MOCR_MLP384_NW, 0, s>>>(p);
+      const bool proj = p.att_hi != nullptr;
+      if (proj && (!p.bproj || (p.att_lo == nullptr) != (p.w1lo == nullptr)))
+        throw std::runtime_error("mlp384 proj: attention planes like the weights' and b_proj");
+      if (p.w1lo) {
+        if (proj) mlp384_kernel<3, true><<<grid, 256, 0, s>>>(p);
+        else mlp384_kernel<3, false><<<grid, 256, 0, s>>>(p);
+      } else {
+        if (proj) mlp384_kernel<1, true><<<grid, 256, 0, s>>>(p);
+        else mlp384_kernel<1, false><<<grid, 256, 0, s>>>(p);
+      }
       break;
     }
     default: throw std::runtime_error("mlp: fused MLP built for C = 96, 192, 384");

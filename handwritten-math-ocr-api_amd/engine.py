@@ -27,7 +27,8 @@ ABI_VERSION = 6
 # kernel-path variants (include/mathocr.h MOCR_VARIANT_*): 0 = production
 VARIANT = {"unfused_attn": 1, "unfused_mlp": 2, "dec_unfolded": 4, "s4_fused_attn": 8, "window_rows": 16, "dec_narrow": 32,
            "logits_f32": 64, "s3_large_batch": 128, "kv_f32": 256,
-           "cross_kv_f24": 512, "unfused_ln_gemm": 1024, "self_kv_f24": 2048, "beam_unfolded": 4096}
+           "cross_kv_f24": 512, "unfused_ln_gemm": 1024, "self_kv_f24": 2048, "beam_unfolded": 4096,
+           "unfused_s3_tail": 8192}
 
 
 class MocrConfig(ctypes.Structure):
@@ -163,6 +164,31 @@ class DecodeResult:
 
 class MocrError(RuntimeError):
     pass
+
+
+def check_ids_tensor(ids_dev, batch: int, max_steps: int, device: int):
+    """Validate the device tensor ``mocr_decode_device`` writes ``batch x (max_steps + 1)``
+    int32 through (``Engine.decode_into``): a raw pointer crosses the C-ABI, so a wrong
+    shape, dtype, layout or device would be an out-of-bounds device write, not an error.
+    Raises ValueError unless ``ids_dev`` is a contiguous int32 CUDA tensor of shape
+    ``[batch, max_steps + 1]`` on HIP device ``device``."""
+    import torch
+    if batch <= 0:
+        raise ValueError("decode_into: no images set (encode a batch first)")
+    if not 1 <= max_steps:
+        raise ValueError("decode_into: max_steps must be >= 1")
+    if not getattr(ids_dev, "is_cuda", False):
+        raise ValueError("decode_into: ids must be a CUDA (HIP device) tensor")
+    if ids_dev.dtype != torch.int32:
+        raise ValueError(f"decode_into: ids must be int32, got {ids_dev.dtype}")
+    want = (batch, max_steps + 1)
+    if tuple(ids_dev.shape) != want:
+        raise ValueError(f"decode_into: ids must be {list(want)} (encoded batch x (max_steps + 1)), "
+                         f"got {list(ids_dev.shape)}")
+    if not ids_dev.is_contiguous():
+        raise ValueError("decode_into: ids must be contiguous")
+    if ids_dev.device.index != device:
+        raise ValueError(f"decode_into: ids are on cuda:{ids_dev.device.index}, the engine on device {device}")
 
 
 class Engine:
@@ -311,7 +337,10 @@ class Engine:
 
     def decode_into(self, ids_dev, max_steps=150, stop="batch") -> int:
         """Decode and write ids [B, max_steps+1] int32 into a device tensor (e.g. a torch
-        CUDA tensor that is then all-gathered).  Returns the number of steps run."""
+        CUDA tensor that is then all-gathered).  Returns the number of steps run.
+        The C side writes batch x (max_steps + 1) int32 through the raw pointer, so the
+        tensor is checked first (``check_ids_tensor``)."""
+        check_ids_tensor(ids_dev, self.batch, max_steps, self.device)
         n = ctypes.c_int32(0)
         self._check(self.lib.mocr_decode_device(self._h, max_steps, STOP[stop], ctypes.c_void_p(ids_dev.data_ptr()),
                                                 ctypes.byref(n)), "mocr_decode_device")

@@ -128,6 +128,73 @@ def global_stop(ids, eos: int):
     return ids[:, :n + 1], n
 
 
+def shard_rows_max(n_total: int, world: int) -> int:
+    """Rows of the largest shard ``shard_bounds`` makes (rank 0's)."""
+    return -(-n_total // world) if n_total > 0 else 0
+
+
+def gather_shards(ids_local, n_total: int, world: int, rank: int, gather, pad_id: int = 0):
+    """Pad-and-trim all-gather of per-rank token streams whose shards may differ by a row.
+
+    The reference accepts any batch size (``src/inference.py:7``), so ``shard_bounds``
+    splits ``n_total`` images into shards of ``m`` or ``m - 1`` rows, while an all-gather
+    (``RcclGroup.gather_ids``, ``gather_ids_host``) moves equal blocks.  Each rank's
+    ``[rows, width]`` ids are padded with ``pad_id`` to ``m`` rows, gathered into
+    ``[world * m, width]`` by ``gather`` (a callable on one equal-shaped block), and each
+    rank's block is trimmed back to its shard; returns the ``[n_total, width]`` ids in
+    global row order.  Equal shards skip the pad and the trim."""
+    import torch
+    a, b = shard_bounds(n_total, world, rank)
+    rows = b - a
+    if ids_local.dim() != 2 or ids_local.shape[0] != rows:
+        raise ValueError(f"rank {rank}'s shard of {n_total} rows over {world} ranks has {rows} rows, "
+                         f"got ids of shape {list(ids_local.shape)}")
+    m = shard_rows_max(n_total, world)
+    if n_total % world == 0:
+        return gather(ids_local)
+    padded = torch.full((m, ids_local.shape[1]), pad_id, dtype=ids_local.dtype, device=ids_local.device)
+    padded[:rows].copy_(ids_local)
+    full = gather(padded)
+    if tuple(full.shape) != (world * m, ids_local.shape[1]):
+        raise ValueError(f"gather returned {list(full.shape)}, expected {[world * m, ids_local.shape[1]]}")
+    parts = []
+    for r in range(world):
+        ra, rb = shard_bounds(n_total, world, r)
+        parts.append(full[r * m:r * m + (rb - ra)])
+    return torch.cat(parts, 0)
+
+
+def decode_sharded(engine, images, n_total: int, world: int, rank: int, gather, max_steps: int = 150,
+                   stop: str = "batch"):
+    """One rank's part of an image-parallel greedy decode of an ``n_total``-image batch.
+
+    ``images``: this rank's shard (rows ``shard_bounds(n_total, world, rank)`` of the global
+    batch, host array or device tensor) for ``engine``; ``gather``: the all-gather of one
+    equal-shaped id block (``RcclGroup.gather_ids`` on device memory, or
+    ``lambda t: gather_ids_host(t.cpu(), world)``).  The shard decodes ``stop="none"``
+    into a device buffer padded to the largest shard's rows (``Engine.decode_into``), the
+    blocks are gathered and trimmed (``gather_shards``), and with ``stop="batch"`` the
+    reference's batch-global stop is applied over the whole gathered batch
+    (``global_stop``, SURVEY §8(e) option 2).  Returns ``(ids [n_total, n + 1], n)`` on
+    every rank."""
+    import torch
+    if stop not in ("batch", "none"):
+        raise ValueError("stop must be 'batch' or 'none'")
+    a, b = shard_bounds(n_total, world, rank)
+    if len(images) != b - a:
+        raise ValueError(f"rank {rank}'s shard is rows [{a}, {b}) of {n_total}, got {len(images)} images")
+    dev = torch.device("cuda", engine.device)
+    m = shard_rows_max(n_total, world)
+    buf = torch.full((m, max_steps + 1), engine.pad, dtype=torch.int32, device=dev)
+    if b > a:
+        engine.encode(images)
+        engine.decode_into(buf[:b - a], max_steps=max_steps, stop="none")
+    ids = gather_shards(buf[:b - a], n_total, world, rank, gather, pad_id=engine.pad)
+    if stop == "none":
+        return ids, max_steps
+    return global_stop(ids, engine.eos)
+
+
 def gather_ids_host(ids_local, world: int, group=None):
     """All-gather equal-shaped per-rank CPU id tensors over a host process group (gloo)
     and concatenate them in rank order (multi-process CPU tests)."""

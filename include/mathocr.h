@@ -95,8 +95,11 @@ enum {
                                      /* mlp.hip's lngemm384_kernel                                   */
   MOCR_VARIANT_SELF_KV_F24 = 2048,   /* bf16x3 engines: the self-attention cache in fp24 instead of  */
                                      /* int16 with one scale per (row, head, key) over its 32 values */
-  MOCR_VARIANT_BEAM_UNFOLDED = 4096  /* beam search on round 2's projection+attention step (fp32     */
+  MOCR_VARIANT_BEAM_UNFOLDED = 4096, /* beam search on round 2's projection+attention step (fp32    */
                                      /* K/V, row GEMMs) instead of the folded wide-tile step         */
+  MOCR_VARIANT_UNFUSED_S3_TAIL = 8192 /* Swin stage 3 at >= 128 images: the attention output         */
+                                     /* projection as its own residual-add GEMM in front of the      */
+                                     /* fused MLP, instead of inside it (mlp.hip mlp384_kernel PROJ) */
 };
 
 /* Greedy stopping rule (src/inference.py:23-25). */

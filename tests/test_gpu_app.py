@@ -69,3 +69,49 @@ def test_load_model_checkpoint_file(pkg, golden, tmp_path):
     res = eng.decode(max_steps=m["steps"], stop="batch")
     eng.close()
     np.testing.assert_array_equal(res.ids, g["ids"])
+
+
+def test_predict_microbatch_on_engine(pkg, golden):
+    """VERDICT r05 item 7 on the GPU: 8 concurrent /predict requests are decoded as ONE
+    engine call, and each returns what im2latex.predict returns for its image alone;
+    then 8 copies of the serving fixture's image through the micro-batcher return the
+    reference's own formula and confidence (``serve96x320_eos``, made by the reference's
+    ``app/src/im2latex.py``)."""
+    import threading
+    from fastapi.testclient import TestClient
+    from PIL import Image
+    from oracle.gen_golden import apply_eos_boost
+    appmod = importlib.import_module("handwritten-math-ocr-api_amd.app.main")
+    vocab, idx2char = pkg.synth.synthetic_vocab()
+    m = golden("serve96x320_eos")["meta"]
+    eng = pkg.Engine(img_hw=(96, 320), max_batch=8, precision="bf16x3")
+    eng.load_weights(apply_eos_boost(pkg.synth.make_weights(m["seed"], m["variant"]), m["eos_boost"]))
+    pngs = [_png(i) for i in range(8)]
+    single = [pkg.im2latex.predict(eng, pkg.preprocess.preprocess_image(Image.open(io.BytesIO(p))), vocab, idx2char)
+              for p in pngs]
+    st = appmod.State(eng, vocab, idx2char, batch_window_ms=5000, max_batch=8)
+    client = TestClient(appmod.create_app(st))
+    out = [None] * 8
+
+    def one(i):
+        out[i] = client.post("/predict", files={"file": (f"{i}.png", pngs[i], "image/png")})
+
+    th = [threading.Thread(target=one, args=(i,)) for i in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert all(r is not None and r.status_code == 200 for r in out), [r and r.text for r in out]
+    assert [r.json()["formula"] for r in out] == [s[0] for s in single]
+    np.testing.assert_allclose([r.json()["confidence"] for r in out], [s[1] for s in single], rtol=1e-6)
+    assert st.batcher.batch_sizes == [8]
+    # the fixture image, 8 requests at once, straight into the batcher
+    img = pkg.synth.make_images(1, m["H"], m["W"], m["img_seed"], m["img_kind"])
+    futs = [st.batcher.submit(img) for _ in range(8)]
+    res = [f.result(120) for f in futs]
+    assert st.batcher.batch_sizes == [8, 8]
+    for formula, conf in res:
+        assert formula == m["formula"]
+        assert conf == pytest.approx(m["confidence"], rel=1e-4, abs=1e-7)
+    st.close()
+    eng.close()

@@ -53,7 +53,7 @@ def test_encoder_stages_match_oracle(pkg, g384):
 
 @pytest.mark.parametrize("variant", [(), ("unfused_attn",), ("unfused_attn", "unfused_mlp"), ("s4_fused_attn",),
                                      ("window_rows",), ("unfused_attn", "window_rows"), ("s3_large_batch",),
-                                     ("s3_large_batch", "unfused_mlp"), ("s3_large_batch", "unfused_ln_gemm"),
+                                     ("s3_large_batch", "unfused_mlp"), ("s3_large_batch", "unfused_ln_gemm"), ("s3_large_batch", "unfused_s3_tail"),
                                      ("unfused_ln_gemm",)])
 def test_bf16x3_encoder_stages_match_oracle(pkg, golden, variant):
     """bf16x3 encoder stage by stage: the fused stage-1/2 attention half (wattn.hip) and

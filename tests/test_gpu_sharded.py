@@ -41,6 +41,24 @@ def _worker(rank, world, port, q, stop="none"):
         from oracle.gen_golden import apply_eos_boost
         g = load_golden("g96x320_b4_eos")
         m = g["meta"]
+        if stop == "ragged":
+            # the product path for any B: 3 of the fixture's rows over 2 ranks (2 + 1), each
+            # rank decoding its shard into a padded device buffer, the pad-and-trim gather,
+            # then the batch-global stop over the whole gathered batch (parallel.decode_sharded)
+            n = 3
+            a, b = pkg.parallel.shard_bounds(n, world, rank)
+            imgs = pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m["img_kind"])[a:b]
+            eng = pkg.Engine(img_hw=(m["H"], m["W"]), max_batch=b - a, precision="bf16x3", device=0)
+            eng.load_weights(apply_eos_boost(pkg.synth.make_weights(m["seed"], m["variant"]), m["eos_boost"]))
+            ids, n_steps = pkg.parallel.decode_sharded(
+                eng, imgs, n, world, rank, lambda t: pkg.parallel.gather_ids_host(t.cpu(), world),
+                max_steps=m["steps"], stop="batch")
+            eng.close()
+            if rank == 0:
+                q.put(("ok", (ids.cpu().numpy(), n_steps)))
+            dist.barrier()
+            dist.destroy_process_group()
+            return
         a, b = pkg.parallel.shard_bounds(m["B"], world, rank)
         imgs = pkg.synth.make_images(m["B"], m["H"], m["W"], m["img_seed"], m["img_kind"])[a:b]
         eng = pkg.Engine(img_hw=(m["H"], m["W"]), max_batch=b - a, precision="bf16x3", device=0)
@@ -179,3 +197,17 @@ def test_bench_two_ranks_torchrun():
     assert len(out["rank_elapsed_s"]["all"]) == 2 and out["rank_elapsed_s"]["max"] * 1e3 / out["steps"] == \
         pytest.approx(out["ms_per_step"])
     assert out["config"]["gather"] in ("rccl (mocr_group_gather_ids)", "gloo host (ranks share a device)")
+
+
+def test_uneven_shards_decode_sharded(pkg, golden):
+    """shards that differ by a row have a product path.  Rows 0-2 of
+    the 96x320 EOS fixture over 2 ranks (2 + 1 images) through ``parallel.decode_sharded``:
+    padded device buffers, the pad-and-trim gather, the batch-global stop over the 3 rows.
+    Rows are independent, so the result is the fixture's rows 0-2 cut at the step where the
+    last of THEM produced EOS (``global_stop`` of the fixture's own columns)."""
+    g = golden("g96x320_b4_eos")
+    ids, n = _run_shards("ragged")
+    # the fixture's ids run to its own 4-row stop; the 3-row stop comes no later
+    ref, n_ref = pkg.parallel.global_stop(g["ids"][:3], pkg.synth.EOS_ID)
+    assert n == n_ref and ids.shape == (3, n_ref + 1), (ids.shape, n, n_ref)
+    np.testing.assert_array_equal(ids, ref)

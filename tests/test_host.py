@@ -194,3 +194,33 @@ def test_global_stop_over_shards(pkg):
     ids[1, 6] = 7  # row 1 never finishes: no stop
     out, n = pkg.parallel.global_stop(ids, eos)
     assert n == 8 and out.shape == (3, 9)
+
+
+def test_decode_into_tensor_checks(pkg):
+    """``Engine.decode_into`` hands a raw device pointer to
+    ``mocr_decode_device``, which writes batch x (max_steps + 1) int32 through it; the
+    tensor's shape, dtype, layout and device are checked before the call."""
+    import torch
+
+    class FakeCuda:  # the attributes check_ids_tensor reads, as a CUDA tensor has them
+        def __init__(self, shape, dtype=torch.int32, contiguous=True, index=0):
+            self.shape, self.dtype, self.is_cuda = shape, dtype, True
+            self._c, self.device = contiguous, torch.device("cuda", index)
+
+        def is_contiguous(self):
+            return self._c
+
+    check = pkg.engine.check_ids_tensor
+    check(FakeCuda((4, 9)), 4, 8, 0)  # accepted
+    bad = [
+        (torch.zeros(4, 9, dtype=torch.int32), 4, 8, 0),   # host tensor
+        (FakeCuda((4, 9), dtype=torch.int64), 4, 8, 0),    # dtype
+        (FakeCuda((4, 8)), 4, 8, 0),                       # too narrow: the C side writes 9 columns
+        (FakeCuda((3, 9)), 4, 8, 0),                       # fewer rows than the encoded batch
+        (FakeCuda((4, 9), contiguous=False), 4, 8, 0),     # strided
+        (FakeCuda((4, 9), index=1), 4, 8, 0),              # another device
+        (FakeCuda((0, 9)), 0, 8, 0),                       # nothing encoded
+    ]
+    for args in bad:
+        with pytest.raises(ValueError):
+            check(*args)

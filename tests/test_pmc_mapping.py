@@ -79,3 +79,20 @@ def test_unfused_ln_gemm_and_the_quantisation_pass(tmp_path):
     assert cls["s3.ln1"]["launches"] == 6 and cls["s3.qkv"]["launches"] == 6
     assert cls["merge1.ln"]["launches"] == 1 and "s3.lnqkv" not in cls
     assert cls["memkv(i16)"]["launches"] == 1
+
+
+def test_stage3_block_tail_maps_to_s3_tail(tmp_path):
+    """Round 6: stage 3 on the fused attention (no proj) and the block-tail kernel
+    (mlp384_kernel PROJ: proj + residual + norm2 + MLP), two dispatches per block."""
+    tool = load_tool()
+    k = bench_dispatches()
+    a = k.index("mocr::lngemm384_kernel<3, 2>", k.index("mocr::ln_group_kernel<64, 12, 2>"))  # stage 3's first block
+    b = k.index("mocr::ln_group_kernel<64, 24, 2>")  # merge 3
+    names = k[:a] + ["mocr::swin_attn_noproj_kernel<384, 3, 3, 12, 2>", "mocr::mlp384_kernel<3, true, 4>"] * 6 + k[b:]
+    write_csv(tmp_path / "f.csv", names, 1.0)
+    write_csv(tmp_path / "w.csv", names, 1.0)
+    tool.main(str(tmp_path / "f.csv"), str(tmp_path / "w.csv"), str(tmp_path / "o.json"))
+    cls = json.load(open(tmp_path / "o.json"))["classes"]
+    assert cls["s3.attn"]["launches"] == 6 and "noproj" in cls["s3.attn"]["kernel"]
+    assert cls["s3.tail"]["launches"] == 6 and "mlp384_kernel<3, true" in cls["s3.tail"]["kernel"]
+    assert "s3.proj" not in cls and "s3.mlp" not in cls and cls["merge1"]["launches"] == 1

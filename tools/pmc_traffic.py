@@ -5,8 +5,12 @@
     python tools/pmc_traffic.py F/run_counter_collection.csv W/run_counter_collection.csv OUT.json [STEPS [BATCH]]
 
 Corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts 64 B per 128-B request for
-wide (16 B/lane) streaming reads on gfx950, so it is doubled; WRITE_SIZE is taken as is
-(exact for 16 B/lane stores, uncalibrated for the 2-4 B/lane epilogue stores here).
+wide (16 B/lane) streaming reads on gfx950, so it is doubled; WRITE_SIZE is taken as is.
+Round 6 calibrated both on the decode step's own access patterns (tools/fetch_calib.hip,
+profiles/r06/fetch_calib.md): 16-, 8- and 4-B lane loads and the fold GEMMs' 64-B row
+segments all reach L2's fabric side as 128-B requests (TCC_EA0_RDREQ_128B), which gfx950's
+FETCH_SIZE formula tallies at 64 B (TCC_BUBBLE reads 0), so x2 holds for every read here;
+WRITE_SIZE is exact for 16-, 4-B and the V4 epilogue's 128-B-row stores.
 Both counters are in KiB.  Encoder dispatches are mapped to the engine's kernel classes
 (engine.hip encode()) by their order in one encode; every dispatch after the encoder
 (``profile_encoder.py --decode-steps N``: the embedding kernel, then N graph-captured
@@ -18,18 +22,22 @@ import json
 import sys
 
 
-def classes_in_order(mlp_fused=(), attn_fused=(), attn_noproj=(), lnqkv=(), lnmerge=()):
+def classes_in_order(mlp_fused=(), attn_fused=(), attn_noproj=(), lnqkv=(), lnmerge=(), tail=()):
     """Encoder dispatch classes in launch order; stages in `mlp_fused` run norm2 + MLP as one
     kernel (mlp.hip) instead of layernorm, fc1, fc2, stages in `attn_fused` run norm1 +
     qkv + W-MSA + proj as one kernel (wattn.hip), stages in `attn_noproj` norm1 + qkv +
     W-MSA as one kernel, then the proj GEMM; stages in `lnqkv` norm1 + qkv as one kernel
-    (mlp.hip lngemm384_kernel), merges in `lnmerge` gather + norm + reduction as one."""
+    (mlp.hip lngemm384_kernel), merges in `lnmerge` gather + norm + reduction as one, stages in
+    `tail` (with `attn_noproj`) proj + residual + norm2 + MLP as one (mlp384_kernel PROJ)."""
     names = ["split(weights)", "split(kv-weights)", "stem"]
     depth = (2, 2, 6, 2)
     for s in range(4):
         for _ in range(depth[s]):
             if s + 1 in attn_fused:
                 names += [f"s{s+1}.attn"]
+            elif s + 1 in attn_noproj and s + 1 in tail:
+                names += [f"s{s+1}.attn", f"s{s+1}.tail"]
+                continue
             elif s + 1 in attn_noproj:
                 names += [f"s{s+1}.attn", f"s{s+1}.proj"]
             elif s + 1 in lnqkv:
@@ -66,7 +74,8 @@ def main(fetch_csv, write_csv, out, decode_steps=0, batch=0):
     n_lng = sum("lngemm384_kernel" in k for k in kn)  # 6 stage-3 blocks and / or merge 1
     lnqkv = [3] if n_lng >= 6 else []
     lnmerge = [1] if n_lng in (1, 7) else []
-    names = with_memkv24(classes_in_order(fused, afused, anoproj, lnqkv, lnmerge), kn)
+    tail = [3] if any("mlp384_kernel<" in k and ", true" in k for k in kn) else []
+    names = with_memkv24(classes_in_order(fused, afused, anoproj, lnqkv, lnmerge, tail), kn)
     # load-time bf16 splits before the stem: weights, kv-weights, and (bf16x3) the folded
     # decoder weights; fp32 mode has none
     n_split = next(i for i, k in enumerate(kn) if "stem" in k)
