@@ -19,15 +19,8 @@ constexpr int kHeadDim = 32;   // Swin and decoder head dim (96/3 ... 768/24; 25
 // A 16-B row slice the greedy decode streams once per step (cross-attention K/V, the
 // self-attention cache): a non-temporal load, so that the K/V streams do not evict the
 // decoder weights and activations that every step re-reads from L2 / the Infinity Cache.
-#ifndef MOCR_KV_NT
-#define MOCR_KV_NT 1
-#endif
 __device__ __forceinline__ floatx4 ld_stream4(const float* p) {
-#if MOCR_KV_NT
   return __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(p));
-#else
-  return *reinterpret_cast<const floatx4*>(p);
-#endif
 }
 
 // fp24 K/V storage of the greedy decode (bf16x3 engines): an fp32 rounded to nearest at
@@ -51,11 +44,7 @@ __device__ __forceinline__ floatx4 fp24_unpack4(u32x3 w) {
 // the 4 elements e .. e + 3 (e % 4 == 0) of a packed buffer
 __device__ __forceinline__ floatx4 ld_stream_fp24x4(const uint8_t* base, size_t e) {
   const u32x3* p = reinterpret_cast<const u32x3*>(base + 3 * e);
-#if MOCR_KV_NT
   return fp24_unpack4(__builtin_nontemporal_load(p));
-#else
-  return fp24_unpack4(*p);
-#endif
 }
 __device__ __forceinline__ void st_fp24x4(uint8_t* base, size_t e, const floatx4& v) {
   const uint32_t r0 = fp24_bits(v[0]), r1 = fp24_bits(v[1]), r2 = fp24_bits(v[2]), r3 = fp24_bits(v[3]);
@@ -72,11 +61,7 @@ __device__ __forceinline__ void st_fp24x4(uint8_t* base, size_t e, const floatx4
 __device__ __forceinline__ floatx4 ld_stream_i16x4(const int16_t* base, size_t e) {
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
   const u32x2* p = reinterpret_cast<const u32x2*>(base + e);
-#if MOCR_KV_NT
   const u32x2 w = __builtin_nontemporal_load(p);
-#else
-  const u32x2 w = *p;
-#endif
   return floatx4{(float)(int16_t)(w[0] & 0xffffu), (float)((int32_t)w[0] >> 16), (float)(int16_t)(w[1] & 0xffffu),
                  (float)((int32_t)w[1] >> 16)};
 }

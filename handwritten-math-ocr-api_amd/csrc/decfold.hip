@@ -297,9 +297,6 @@ __device__ unsigned long long g_attn_ts[8192 * 8];
 // head, key) over its 32 values (the key's scale multiplies its score, the value's its
 // softmax weight), the newest key / value quantised here by the same rule.
 // NW waves (8 key rows each per pass; the selection runs on all 64 NW threads).
-#ifndef MOCR_XATTN_PROBE
-#define MOCR_XATTN_PROBE 0
-#endif
 template <bool SELF, bool ZS, bool SEL, int NIT, int KVF, int NW, bool SLOT = false>
 __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   MOCR_ATS(0, __builtin_amdgcn_s_memrealtime());
@@ -328,9 +325,7 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   static_assert(!SLOT || (SELF && !SEL), "slot tables: the self-attention of beam hypotheses");
   // the K/V row: this decoder row, its image's memory row (cross-attention of beam
   // hypotheses: mem_div of them per image), or per key its slot row (SLOT, below)
-  // MOCR_XATTN_PROBE (timing probe, wrong results): every row's cross-attention reads
-  // memory row 0's K/V, which then stays in L2 (what the K/V stream costs in the pipeline)
-  const int mb = SELF ? b : (MOCR_XATTN_PROBE ? 0 : (p.mem_div > 1 ? b / p.mem_div : b));
+  const int mb = SELF ? b : (p.mem_div > 1 ? b / p.mem_div : b);
   auto row_base = [&](int r) -> size_t {
     return KVF ? (size_t)r * p.f24_b + (size_t)h * p.f24_h + li * 4 : (size_t)r * p.kv_b_stride + cc;
   };
@@ -547,136 +542,6 @@ __global__ void __launch_bounds__(256) dec_foldattn_kernel(FoldAttnParams p) {
   MOCR_ATS(6, __builtin_amdgcn_s_memrealtime());
 }
 
-// Cross-attention on int16 K/V with 16-B loads: 4 lanes per key row (8 columns each), 16
-// key rows per wave instruction (dec_foldattn_kernel: 8 lanes of 8-B loads, 8 rows). The
-// same arithmetic per score and per output column, summed in a different order.
-// Measured slower: the decode step 440 -> 469 us at 512 rows (2 or 3 waves), the extra
-// cross-lane sums and registers outweigh the halved load count (profiles/r05/r07u/).
-#ifndef MOCR_XATTN_LPR4  // A/B builds: 1 / 2 -> dec_xattn16_kernel on 2 / 3 waves
-#define MOCR_XATTN_LPR4 0
-#endif
-__device__ __forceinline__ void ld_stream_i16x8(const int16_t* base, size_t e, floatx4& a, floatx4& b) {
-  const uint4 w = *reinterpret_cast<const uint4*>(base + e);
-  a = floatx4{(float)(int16_t)(w.x & 0xffffu), (float)((int32_t)w.x >> 16), (float)(int16_t)(w.y & 0xffffu),
-              (float)((int32_t)w.y >> 16)};
-  b = floatx4{(float)(int16_t)(w.z & 0xffffu), (float)((int32_t)w.z >> 16), (float)(int16_t)(w.w & 0xffffu),
-              (float)((int32_t)w.w >> 16)};
-}
-// over the 16 key-row groups of a wave (lanes i, i +- 4, .. within a row by row_ror, then the
-// other rows): every lane of a column gets the group's max / a sum
-__device__ __forceinline__ float xmax4_8_16_32(float x) { return xmax8_16_32(fmaxf(x, dpp<0x124>(x))); }
-__device__ __forceinline__ float xsum4_8_16_32(float x) { return xsum8_16_32(x + dpp<0x124>(x)); }
-
-template <bool ZS, int NIT, int NW>
-__global__ void __launch_bounds__(256) dec_xattn16_kernel(FoldAttnParams p) {
-  constexpr int LPR = 4, RPW = 16;
-  __shared__ floatx4 po[NW][8];
-  __shared__ float pm[NW], ps[NW];
-  const int b = blockIdx.x;
-  const int h = blockIdx.y;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int rsub = lane / LPR;
-  const int li = lane % LPR;
-  const int cc = h * 32 + li * 8;  // this lane's 8 columns of the head
-  const int t = p.t;
-  const int n = p.n;
-  const int m_first = wave * RPW + rsub;
-  const int mb = p.mem_div > 1 ? b / p.mem_div : b;
-  const size_t kvb = (size_t)mb * p.f24_b + (size_t)h * p.f24_h + li * 8;
-  floatx4 kk[NIT][2], vv[NIT][2];
-#pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int m = m_first + it * NW * RPW;
-    const size_t o = kvb + (size_t)(m < n ? m : 0) * 32;
-    ld_stream_i16x8(p.K16, o, kk[it][0], kk[it][1]);
-    ld_stream_i16x8(p.V16, o, vv[it][0], vv[it][1]);
-  }
-  floatx4 zv[2], sv[2], cv[2];
-  const float* zr = p.z + (size_t)b * p.z_ld + cc;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    zv[j] = *reinterpret_cast<const floatx4*>(zr + 4 * j);
-    if constexpr (ZS) {
-      sv[j] = *reinterpret_cast<const floatx4*>(p.s + cc + 4 * j);
-      cv[j] = *reinterpret_cast<const floatx4*>(p.c + cc + 4 * j);
-    }
-  }
-  if constexpr (ZS) {
-    float mean, rstd;
-    row_stats_16lanes(p.z_stats + (size_t)b * 2 * kSlices, lane & 15, mean, rstd);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) zv[j][e] = fmaf(rstd, fmaf(-mean, sv[j][e], zv[j][e]), cv[j][e]);
-  }
-  floatx4 q[2], vs[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    q[j] = zv[j] * *reinterpret_cast<const floatx4*>(p.Ks + (size_t)mb * p.s_b + cc + 4 * j);
-    vs[j] = *reinterpret_cast<const floatx4*>(p.Vs + (size_t)mb * p.s_b + cc + 4 * j);
-  }
-  const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
-  float sc[NIT];
-  float mx = -INFINITY;
-#pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int m = m_first + it * NW * RPW;
-    vv[it][0] = m < n ? vv[it][0] : zero;
-    vv[it][1] = m < n ? vv[it][1] : zero;
-    float s = q[0][0] * kk[it][0][0];
-#pragma unroll
-    for (int e = 1; e < 8; ++e) s = fmaf(q[e >> 2][e & 3], kk[it][e >> 2][e & 3], s);
-    s += dpp<0xB1>(s);  // the key row's 4 lanes
-    s += dpp<0x4E>(s);
-    s *= kAttnScale;
-    sc[it] = m < n ? s : -INFINITY;
-    mx = fmaxf(mx, sc[it]);
-  }
-  mx = xmax4_8_16_32(mx);
-  float sum = 0.f;
-  floatx4 o[2] = {zero, zero};
-  if (mx != -INFINITY) {
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const float e = __expf(sc[it] - mx);
-      sum += e;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) o[j][c] = fmaf(e, vv[it][j][c], o[j][c]);
-    }
-  }
-  sum = xsum4_8_16_32(sum);
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) o[j][c] = xsum4_8_16_32(o[j][c]);
-  if (rsub == 0) {
-    po[wave][2 * li] = o[0] * vs[0];
-    po[wave][2 * li + 1] = o[1] * vs[1];
-    if (li == 0) {
-      pm[wave] = mx;
-      ps[wave] = sum;
-    }
-  }
-  __syncthreads();
-  if (tid < 32 && !dec_skip(p.st, t)) {
-    float m = pm[0];
-#pragma unroll
-    for (int w = 1; w < NW; ++w) m = fmaxf(m, pm[w]);
-    float num = 0.f, den = 0.f;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      const float f = pm[w] == -INFINITY ? 0.f : __expf(pm[w] - m);
-      num = fmaf(po[w][tid / 4][tid % 4], f, num);
-      den = fmaf(ps[w], f, den);
-    }
-    p.out[(size_t)b * kD + h * 32 + tid] = num * __builtin_amdgcn_rcpf(den);
-  }
-}
-
 // ------------------------------------------------------------------ load-time folding
 // out[i, j] = sum_k A[i, k] g[k] Bm[k sbk + j sbj] (+ add_row[i] + add_col[j]) in fp64,
 // rounded once to fp32; Bm null: out = A diag(g).
@@ -755,12 +620,9 @@ void launch_dec_foldattn(const FoldAttnParams& p, bool self_attn, hipStream_t s)
   // waves per workgroup: 2 unless the keys exceed 2 x 8 x 10 (tools/attn_ts: the 4-wave
   // kernel's per-wave fixed work -- statistics, unfold, the reductions -- made 8 waves per
   // SIMD VALU-bound: cross 9.9 -> 8.5 us, self at t = 16 6.9 -> 5.4, t = 120 10.8 -> 10.3)
-#ifndef MOCR_ATTN_WAVES
-#define MOCR_ATTN_WAVES 2
-#endif
   // (one wave up to 40 keys: self-attention at t = 16 5.42 -> 4.75 us; equal at t = 60,
   // slower from there and for the 144 memory keys, 8.5 -> 9.3 us)
-  const int nw = p.waves ? p.waves : (p.n > 160 ? 4 : (p.n <= 40 ? 1 : MOCR_ATTN_WAVES));
+  const int nw = p.waves ? p.waves : (p.n > 160 ? 4 : (p.n <= 40 ? 1 : 2));
   if (nw != 1 && nw != 2 && nw != 4) throw std::runtime_error("foldattn: 1, 2 or 4 waves");
   const int nit = (p.n + 8 * nw - 1) / (8 * nw);  // 8 nw key rows per workgroup pass
   const dim3 grid(p.B, kD / 32);
@@ -799,23 +661,6 @@ void launch_dec_foldattn(const FoldAttnParams& p, bool self_attn, hipStream_t s)
     break;
   if ((nw == 2 && nit > 10) || (nw == 1 && nit > 5))
     throw std::runtime_error("foldattn: at most 160 keys on 2 waves, 40 on 1");
-  if (MOCR_XATTN_LPR4 && i16 && nw == 2 && !p.slot_rows) {  // 16 key rows per wave pass
-    if (p.f24_h % 32 != 0 || p.s_b % 8 != 0 || p.z_ld % 8 != 0) throw std::runtime_error("foldattn: int16 K/V alignment");
-    constexpr int W16 = MOCR_XATTN_LPR4 == 2 ? 3 : 2;  // 3 waves: the 144 memory keys in 3 passes
-    const int nit16 = (p.n + 16 * W16 - 1) / (16 * W16);
-#define MOCR_XA(N)                                                          \
-  case N:                                                                   \
-    if (zs) dec_xattn16_kernel<true, N, W16><<<grid, 64 * W16, 0, s>>>(p);  \
-    else dec_xattn16_kernel<false, N, W16><<<grid, 64 * W16, 0, s>>>(p);    \
-    break;
-    switch (nit16) {
-      MOCR_XA(1) MOCR_XA(2) MOCR_XA(3) MOCR_XA(4) MOCR_XA(5)
-      default: throw std::runtime_error("foldattn: at most 160 keys");
-    }
-#undef MOCR_XA
-    MOCR_HIP_CHECK(hipGetLastError());
-    return;
-  }
   if (p.slot_rows) {
     // beam hypotheses' self-attention: the int16 cache (bf16x3 engines) or fp32 (fp32 engines)
     if (!self_attn || p.sel_on || f24 || p.slot_ld < p.n) throw std::runtime_error("foldattn: slot tables need "

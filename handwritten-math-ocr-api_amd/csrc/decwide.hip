@@ -315,15 +315,6 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
 #pragma unroll
       for (int mf = 0; mf < MF; ++mf) {
         floatx4 x = ra[s % NR][h][mf];
-#ifdef MOCR_FOLD_NOXFORM  // timing probe: no LN / unfold transform, no split (wrong results)
-        {
-          const int lt = q + 16 * (h * 2 + (c >> 1));
-          char* f = a_s + mf * 2048 + lt * 16 + (c & 1) * 8;
-          *reinterpret_cast<uint2*>(f) = make_uint2(__float_as_uint(x[0]), __float_as_uint(x[1]));
-          *reinterpret_cast<uint2*>(f + 1024) = make_uint2(__float_as_uint(x[2]), __float_as_uint(x[3]));
-          continue;
-        }
-#endif
         if ((S1 && in1) || (S2 && !YT && !in1)) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -624,13 +615,8 @@ void launch_fw_nw(const FoldGemmParams& p, hipStream_t s) {
 // (FFN at 256 rows 9.1 -> 7.5 us), 4 for the logits (10.8 vs 11.8 us)
 template <int BM, int BN, bool X3, bool LOGITS>
 void launch_fw(const FoldGemmParams& p, hipStream_t s) {
-#ifndef MOCR_FOLD_WAVES  // A/B builds (tools/build_variant.sh DIR -DMOCR_FOLD_WAVES=4)
-#define MOCR_FOLD_WAVES 8
-#endif
-#ifndef MOCR_LOGITS_WAVES
-#define MOCR_LOGITS_WAVES 4
-#endif
-  if ((p.waves ? p.waves : (LOGITS ? MOCR_LOGITS_WAVES : MOCR_FOLD_WAVES)) == 8)
+  constexpr int kFoldWaves = 8, kLogitsWaves = 4;
+  if ((p.waves ? p.waves : (LOGITS ? kLogitsWaves : kFoldWaves)) == 8)
     launch_fw_nw<BM, BN, X3, LOGITS, 8>(p, s);
   else
     launch_fw_nw<BM, BN, X3, LOGITS, 4>(p, s);
@@ -682,15 +668,7 @@ void launch_foldwide(const FoldGemmParams& p, hipStream_t s) {
         if (x3) launch_fw<16, 32, true, false>(p, s); else launch_fw<16, 32, false, false>(p, s);
       }
     } else {
-#ifndef MOCR_FFN_BN64  // A/B builds: the FFN fold GEMM on 32 x 64 tiles above 256 rows
-#define MOCR_FFN_BN64 0
-#endif
-      // 32 x 64 tiles: half the workgroups (one per CU at 512 rows) and half the A
-      // transform (the unfold runs once per row and column tile), the same k order per
-      // output element (the NW-wave K split does not depend on the tile width)
-      if (MOCR_FFN_BN64 && p.K1 == 512 && p.B > 256 && (p.NY + p.NZ) % 512 == 0) {
-        if (x3) launch_fw<32, 64, true, false>(p, s); else launch_fw<32, 64, false, false>(p, s);
-      } else if (narrow_n) {
+      if (narrow_n) {
         if (x3) launch_fw<32, 16, true, false>(p, s); else launch_fw<32, 16, false, false>(p, s);
       } else {
         if (x3) launch_fw<32, 32, true, false>(p, s); else launch_fw<32, 32, false, false>(p, s);

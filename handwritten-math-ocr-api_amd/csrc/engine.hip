@@ -264,10 +264,6 @@ StageGeom make_win(int H, int W, int C, int heads) {
   return g;
 }
 
-// stage 3 (C = 384) on its fused attention kernel at every batch (see noproj_fused)
-#ifndef MOCR_S3_FUSED_ATTN_LARGE
-#define MOCR_S3_FUSED_ATTN_LARGE 1
-#endif
 
 template <typename T>
 T* dalloc(size_t n) {
@@ -1030,8 +1026,11 @@ struct mocr_engine {
         const SwinBlockW& w = lay->blocks[bi];
         // W_qkv fragments: the fused attention kernels of stages 1-3 (stage 4 only under
         // MOCR_VARIANT_S4_FUSED_ATTN), W_proj at C = 96, 192
-        const bool qkv_frags = attn_fused() && (C != 768 || (cfg.variant & MOCR_VARIANT_S4_FUSED_ATTN));
-        for (int m = qkv_frags ? 0 : 1; m < (swin_attn_fused_supported(C) ? 2 : (qkv_frags ? 1 : 0)); ++m) {
+        // (W_proj's fragments only when the fused attention that reads them runs)
+        const bool need_frag[2] = {attn_fused() && (C != 768 || (cfg.variant & MOCR_VARIANT_S4_FUSED_ATTN)),
+                                   attn_fused() && swin_attn_fused_supported(C)};
+        for (int m = 0; m < 2; ++m) {
+          if (!need_frag[m]) continue;
           FragW& f = swinfrag[bi][m];
           const int N = m == 0 ? 3 * C : C;
           if (!f.hi) {
@@ -1061,9 +1060,8 @@ struct mocr_engine {
           launch_mlp_pack(mp, mlppack[bi], stream);
         }
         // lngemm384's W_qkv image: stage 3's norm1 + qkv runs on it only when its fused
-        // attention kernel does not (MOCR_VARIANT_UNFUSED_ATTN, or a MOCR_S3_FUSED_ATTN_LARGE=0
-        // build at >= 128 images)
-        if (C == 384 && (!attn_fused() || !MOCR_S3_FUSED_ATTN_LARGE) && !(cfg.variant & MOCR_VARIANT_UNFUSED_LN_GEMM)) {
+        // attention kernel does not (MOCR_VARIANT_UNFUSED_ATTN)
+        if (C == 384 && !attn_fused() && !(cfg.variant & MOCR_VARIANT_UNFUSED_LN_GEMM)) {
           if (lngpack.size() <= (size_t)bi) lngpack.resize(bi + 1, nullptr);
           if (!lngpack[bi]) {
             lngpack[bi] = dalloc<char>((size_t)3 * C * C * 2 * (dwl ? 2 : 1));
@@ -1219,11 +1217,9 @@ struct mocr_engine {
   // (round 4): 8.30 vs 8.93 ms per 512-image encode for lngemm384 + the window attention,
   // bench +1 %, and no fp32 QKV round trip through HBM (profiles/r04/r04x).  Round 3 kept it
   // below 128 images (1054 vs 903 us per block at B = 256 with row-major fragments,
-  // profiles/r03/op_times_b256.log).  0: lngemm384 + window attention at >= 128 images.
-  bool noproj_fused(int C, int B) const {
-    return attn_fused() && swin_attn_noproj_supported(C) &&
-           (C != 768 || (cfg.variant & MOCR_VARIANT_S4_FUSED_ATTN)) &&
-           (C != 384 || !s3_large(B) || MOCR_S3_FUSED_ATTN_LARGE);
+  // profiles/r03/op_times_b256.log).
+  bool noproj_fused(int C) const {
+    return attn_fused() && swin_attn_noproj_supported(C) && (C != 768 || (cfg.variant & MOCR_VARIANT_S4_FUSED_ATTN));
   }
   // stage 3's kernels for >= 128 images: the unfused attention (above) and mlp.hip's fused
   // C = 384 MLP, which runs 128 rows per workgroup on all 256 CUs (1152 workgroups at
@@ -1234,7 +1230,7 @@ struct mocr_engine {
   // projection + residual inside the fused MLP kernel (mlp.hip mlp384_kernel PROJ), which
   // takes O from the fused attention's ATT planes in X's row order
   bool s3_tail_fused(int C, int B) const {
-    return C == 384 && bf16_mode() && noproj_fused(C, B) && s3_large(B) && mlp_fused() && mlp_fused_supported(C) &&
+    return C == 384 && bf16_mode() && noproj_fused(C) && s3_large(B) && mlp_fused() && mlp_fused_supported(C) &&
            !(cfg.variant & MOCR_VARIANT_UNFUSED_S3_TAIL);
   }
   int attn_passes() const {
@@ -1355,7 +1351,7 @@ struct mocr_engine {
           ap.wg = wg;
           timed(attn_n[s], 8.0 * rows * C * C + 4.0 * rows * kWinTok * C, 8.0 * rows * C + (dwl ? 4.0 : 2.0) * 4.0 * C * C,
                 [&] { launch_swin_attn_fused(ap, stream); });
-        } else if (b16 && noproj_fused(C, B)) {
+        } else if (b16 && noproj_fused(C)) {
           // norm1 + qkv + W-MSA in one kernel writing the ATT planes (wattn.hip), then proj
           SwinAttnParams ap{};
           ap.X = X;

@@ -28,32 +28,14 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-#ifndef MOCR_GELU_728
-#define MOCR_GELU_728 0
-#endif
 // 2 x GELU(x) = x (1 + erf(x / sqrt 2)) (gemm.hip gelu_fast, A&S 7.1.26, without its factor
 // 0.5): the fused MLP kernels' W2 chunk images hold W2 / 2 (mlp_pack_kernel, pack_img384's
 // W2 image), so GEMM 2 multiplies the same bf16 products -- (2h) (W2 / 2) = h W2 exactly,
-// splits included -- and the outputs are bitwise the unscaled ones, one multiply per
-// hidden value fewer
+// splits included -- and the outputs are bitwise the unscaled ones whenever every W2 plane
+// value is a normal bf16 whose half is normal too (exponent field > 1: half_bf16x2 is then an
+// exact exponent decrement; below that, mostly lo-plane residuals of tiny weights, it halves
+// through fp32 with truncation and FTZ), one multiply per hidden value fewer
 __device__ __forceinline__ float gelu2_erf_fast(float x) {
-  if constexpr (MOCR_GELU_728) {
-    // A&S 7.1.28: erf(z) = 1 - (1 + a1 z + ... + a6 z^6)^-16, |error| <= 3e-7: one
-    // reciprocal and no exp (7.1.26 needs both); GELU's absolute error <= 5e-7
-    const float z = fabsf(x) * 0.70710678118654752440f;
-    float p = fmaf(4.30638e-5f, z, 2.765672e-4f);
-    p = fmaf(p, z, 1.520143e-4f);
-    p = fmaf(p, z, 9.2705272e-3f);
-    p = fmaf(p, z, 4.22820123e-2f);
-    p = fmaf(p, z, 7.05230784e-2f);
-    p = fmaf(p, z, 1.0f);
-    p = p * p;
-    p = p * p;
-    p = p * p;
-    p = p * p;
-    const float e = 1.0f - __builtin_amdgcn_rcpf(p);
-    return x * (1.0f + copysignf(e, x));
-  }
   const float z = fabsf(x) * 0.70710678118654752440f;
   const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
   float poly = fmaf(1.061405429f, t, -1.453152027f);
@@ -186,24 +168,17 @@ __device__ __forceinline__ uint4 half_bf16x8(uint4 v) {
 // LDS by LDS-DMA (dma16: no staging registers) and its residual rows are loaded in the
 // epilogue, 158 VGPRs and no AGPRs instead of 152 + 68 (two waves per SIMD): s1.mlp 4.73 /
 // 4.78 vs 5.36 / 5.40 ms per 512-image encode, bitwise the same memory (profiles/r05/r07e).
-// A/B builds: -DMOCR_S1_MLP_OCC3=0 -> register staging, two waves per SIMD
-#ifndef MOCR_S1_MLP_OCC3
-#define MOCR_S1_MLP_OCC3 1
-#endif
-// The stage-2 kernel (with MOCR_S2_MLP_NWV = 4) on 4-wave workgroups with one LDS buffer
+// The stage-2 kernel on 4-wave workgroups with one LDS buffer
 // filled by LDS-DMA between two barriers: 148 VGPRs and 53 KB, three workgroups per CU
 // (12 waves) instead of one 8-wave workgroup (229 VGPRs, 102 KB): s2.mlp 4.21 / 4.27 vs
 // 4.53 / 4.61 ms per 512-image encode, bitwise the same memory (profiles/r05/r07h).  With
 // register staging the same geometry measured slower (round 5, r06h: 4.9-5.0 vs 4.5 ms).
-// A/B builds: -DMOCR_S2_MLP_DMA=0 -DMOCR_S2_MLP_NWV=8
-#ifndef MOCR_S2_MLP_DMA
-#define MOCR_S2_MLP_DMA 1
-#endif
+// Both run the DMA form (NWV = 4); NWV = 8 keeps round 4's register-staged chunks.
 template <int C, int TT, int NC, int PASSES, int NWV = 8, int NBUF = 2>
 __global__ void __launch_bounds__(64 * NWV)
-__attribute__((amdgpu_waves_per_eu((C == 96 && MOCR_S1_MLP_OCC3) || (C == 192 && MOCR_S2_MLP_DMA) ? (NWV == 4 ? 3 : 1) : 1, 8)))
+__attribute__((amdgpu_waves_per_eu(NWV == 4 ? 3 : 1, 8)))
 mlp_fused_kernel(MlpParams p) {
-  constexpr bool PRERES = !(NWV == 4 && ((C == 96 && MOCR_S1_MLP_OCC3) || (C == 192 && MOCR_S2_MLP_DMA)));
+  constexpr bool PRERES = NWV != 4;
   constexpr bool X3 = PASSES == 3;
   constexpr int PL = X3 ? 2 : 1;
   constexpr int RC = C / 8;  // 16-B chunks per W1 row
@@ -1161,16 +1136,9 @@ void launch_mlp_c(const MlpParams& p, hipStream_t s) {
 // 152 VGPRs: three workgroups per CU, whose LayerNorm prologues and residual epilogues
 // overlap the others' chunk loops) instead of 8 waves with 64-unit chunks (100 KB, 256
 // VGPRs, one per CU): 5.30-5.39 vs 5.72-5.75 ms per 512-image encode (profiles/r05/r06f).
-// A/B builds: -DMOCR_S1_MLP_NWV=8
-#ifndef MOCR_S1_MLP_NWV
-#define MOCR_S1_MLP_NWV 4
-#endif
-// stage 2: 4-wave workgroups of 64 rows, one LDS buffer filled by LDS-DMA (MOCR_S2_MLP_DMA;
-// A/B builds: -DMOCR_S2_MLP_NWV=8 -DMOCR_S2_MLP_DMA=0 -> 8 waves, two register-staged buffers)
-#ifndef MOCR_S2_MLP_NWV
-#define MOCR_S2_MLP_NWV 4
-#endif
-constexpr int kS1MlpNC = MOCR_S1_MLP_NWV == 4 ? 32 : 64;
+// stage 2: 4-wave workgroups of 64 rows, one LDS buffer filled by LDS-DMA
+constexpr int kS1MlpNWV = 4, kS2MlpNWV = 4;
+constexpr int kS1MlpNC = kS1MlpNWV == 4 ? 32 : 64;
 
 }  // namespace
 
@@ -1185,10 +1153,7 @@ void launch_lngemm384(const LnGemm384Params& p, hipStream_t s) {
     throw std::runtime_error("lngemm384: PatchMerging rows must be B x ceil(H/2) x ceil(W/2)");
   // 128 rows per workgroup (2 row tiles per wave, the LN rows in 192 of the 256 arch VGPRs;
   // the prologue spills, the chunk loop does not): 1152 workgroups at B = 256
-#ifndef MOCR_LNG_TT
-#define MOCR_LNG_TT 2
-#endif
-  constexpr int TT = MOCR_LNG_TT;
+  constexpr int TT = 2;
   const unsigned grid = (unsigned)((p.M + 64 * TT - 1) / (64 * TT));
   if (p.wlo)
     lngemm384_kernel<3, TT><<<grid, 256, 0, s>>>(p);
@@ -1235,8 +1200,8 @@ void launch_mlp_fused(const MlpParams& p, hipStream_t s) {
   switch (p.C) {
     // rows per wave 16 TT and hidden chunk NC measured best (TT = 1 at C = 96: 514 vs 420 us
     // per s1 block; TT = 2 at C = 192 spills)
-    case 96: launch_mlp_c<96, 2, kS1MlpNC, MOCR_S1_MLP_NWV>(p, s); break;  // NC: launch_mlp_pack's chunks
-    case 192: launch_mlp_c<192, 1, 32, MOCR_S2_MLP_NWV, MOCR_S2_MLP_NWV == 4 ? 1 : 2>(p, s); break;
+    case 96: launch_mlp_c<96, 2, kS1MlpNC, kS1MlpNWV>(p, s); break;  // NC: launch_mlp_pack's chunks
+    case 192: launch_mlp_c<192, 1, 32, kS2MlpNWV, kS2MlpNWV == 4 ? 1 : 2>(p, s); break;
     case 384: {
       const unsigned grid = (unsigned)((p.M + 127) / 128);
       const bool proj = p.att_hi != nullptr;

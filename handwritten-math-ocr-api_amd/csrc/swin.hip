@@ -55,9 +55,8 @@ struct LnGeom {
   WinGeom win;
 };
 
-#ifndef MOCR_LN_LDS_OUT  // 1: bf16 planes through LDS as whole 16-B lanes (merge2 / merge3 norms
-#define MOCR_LN_LDS_OUT 1  // 408 / 276 -> 304 / 180 us per 512 images, profiles/r05/r07r/)
-#endif
+// bf16 planes leave through LDS as whole 16-B lanes (merge2 / merge3 norms 408 / 276 ->
+// 304 / 180 us per 512 images, profiles/r05/r07r/)
 template <int LPR, int F, int MODE>
 __global__ void __launch_bounds__(256) ln_group_kernel(const float* __restrict__ X, const float* __restrict__ g,
                                                        const float* __restrict__ b, RowOut out, LnGeom geo) {
@@ -134,7 +133,7 @@ __global__ void __launch_bounds__(256) ln_group_kernel(const float* __restrict__
       for (int k = 0; k < 4; ++k) v[e + k] = (v[e + k] - mean) * rstd * gg[k] + bb[k];
     }
   }
-  if (MOCR_LN_LDS_OUT && !out.f32 && out.hi) {
+  if (!out.f32 && out.hi) {
     // the wave's RPW rows are 64 F contiguous outputs: each plane goes through the wave's
     // LDS slice and leaves as whole 16-B lanes (8 bf16), not F / 4 8-B stores per lane
     __shared__ __attribute__((aligned(16))) uint32_t st[4][32 * F];
@@ -197,82 +196,15 @@ void launch_ln_group(const float* X, const float* g, const float* b, const RowOu
 
 // ---------------------------------------------------------------- stem (vectorised)
 // Conv2d(1, 96, 4, 4) + LayerNorm(96): 16 lanes per token, 6 channels per lane whose
-// 6x16 weights stay in registers over a grid-stride loop of tokens; the token's 4x4
-// patch is 4 float4 loads (shared by the 16 lanes); LayerNorm over the 16 lanes.
-__global__ void __launch_bounds__(256) stem16_kernel(const float* __restrict__ img, const float* __restrict__ w,
-                                                     const float* __restrict__ bias, const float* __restrict__ g,
-                                                     const float* __restrict__ beta, float* __restrict__ X, long ntok,
-                                                     int H, int W, int Hs, int Ws) {
-  const int lane = threadIdx.x & 63;
-  const int gi = lane & 15;
-  const int c0 = gi * 6;
-  float wr[6][16], br[6], gr[6], be[6];
-#pragma unroll
-  for (int c = 0; c < 6; ++c) {
-#pragma unroll
-    for (int k4 = 0; k4 < 4; ++k4) {  // a channel's 16 weights as 4 float4
-      const floatx4 t = *reinterpret_cast<const floatx4*>(w + (c0 + c) * 16 + 4 * k4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) wr[c][4 * k4 + e] = t[e];
-    }
-    br[c] = bias[c0 + c];
-    gr[c] = g[c0 + c];
-    be[c] = beta[c0 + c];
-  }
-  const long step = (long)gridDim.x * 16;
-  for (long tok = (long)blockIdx.x * 16 + (threadIdx.x >> 4); tok < ntok; tok += step) {
-    const int b = (int)(tok / ((long)Hs * Ws));
-    const int rem = (int)(tok - (long)b * Hs * Ws);
-    const int y = rem / Ws;
-    const int x = rem - y * Ws;
-    const float* src = img + ((size_t)b * H + 4 * y) * W + 4 * x;
-    float px[16];
-#pragma unroll
-    for (int ky = 0; ky < 4; ++ky) {
-      const floatx4 t = *reinterpret_cast<const floatx4*>(src + (size_t)ky * W);
-      px[4 * ky] = t[0];
-      px[4 * ky + 1] = t[1];
-      px[4 * ky + 2] = t[2];
-      px[4 * ky + 3] = t[3];
-    }
-    float v[6];
-    float s = 0.f;
-#pragma unroll
-    for (int c = 0; c < 6; ++c) {
-      float acc = 0.f;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) acc = fmaf(wr[c][k], px[k], acc);
-      v[c] = acc + br[c];
-      s += v[c];
-    }
-    s = row_sum<16>(s);  // the token's 16 lanes, by DPP (lanes.h; the xor butterfly's pairs)
-    const float mean = s / 96.f;
-    float q = 0.f;
-#pragma unroll
-    for (int c = 0; c < 6; ++c) {
-      const float d = v[c] - mean;
-      q += d * d;
-    }
-    q = row_sum<16>(q);
-    const float rstd = 1.0f / sqrtf(q / 96.f + 1e-5f);
-    float o[6];
-#pragma unroll
-    for (int c = 0; c < 6; ++c) o[c] = (v[c] - mean) * rstd * gr[c] + be[c];
-    float* dst = X + (size_t)tok * 96 + c0;
-    *reinterpret_cast<float2*>(dst) = make_float2(o[0], o[1]);
-    *reinterpret_cast<float2*>(dst + 2) = make_float2(o[2], o[3]);
-    *reinterpret_cast<float2*>(dst + 4) = make_float2(o[4], o[5]);
-  }
-}
-
+// 6x16 weights stay in registers over a grid-stride loop of tokens; LayerNorm over the 16
+// lanes.
 // The same per-token arithmetic with the patch loads spread over the wave: each lane loads
 // one float4 (a patch row) of 16 consecutive tokens, one sweep ahead, and the four 16-lane
 // groups read their tokens' patches back from the wave's 1 KB LDS slice. The 4-float4-per-
 // lane form keeps one wave's 4 patches (256 B) in flight per HBM round trip; this one 16
 // patches plus the next sweep's 16.
-#ifndef MOCR_STEM_LDS_OUT  // 1: X leaves through an LDS slice as whole 16-B lanes (596 -> 457 us
-#define MOCR_STEM_LDS_OUT 1  // per 512 images, profiles/r05/r07q/); 0: three 8-B stores per lane
-#endif
+// X leaves through an LDS slice as whole 16-B lanes (596 -> 457 us per 512 images against
+// three 8-B stores per lane, profiles/r05/r07q/).
 template <int DEPTH>
 __global__ void __launch_bounds__(256) stem16w_kernel(const float* __restrict__ img, const float* __restrict__ w,
                                                       const float* __restrict__ bias, const float* __restrict__ g,
@@ -284,7 +216,7 @@ __global__ void __launch_bounds__(256) stem16w_kernel(const float* __restrict__ 
   const int grp = lane >> 4;
   const int c0 = gi * 6;
   __shared__ floatx4 patch[4][64];  // per wave: 16 tokens x 4 patch rows
-  __shared__ __attribute__((aligned(16))) float xout[4][MOCR_STEM_LDS_OUT ? 16 * 96 : 4];  // per wave: 16 tokens of X
+  __shared__ __attribute__((aligned(16))) float xout[4][16 * 96];  // per wave: 16 tokens of X
   float wr[6][16], br[6], gr[6], be[6];
 #pragma unroll
   for (int c = 0; c < 6; ++c) {
@@ -326,7 +258,6 @@ __global__ void __launch_bounds__(256) stem16w_kernel(const float* __restrict__ 
 #pragma unroll 1
     for (int j = 0; j < 4; ++j) {
       const int tw = 4 * j + grp;  // token within the wave's 16
-      const long tok = t0 + tw;
       float px[16];
 #pragma unroll
       for (int ky = 0; ky < 4; ++ky) {
@@ -359,18 +290,11 @@ __global__ void __launch_bounds__(256) stem16w_kernel(const float* __restrict__ 
       float o[6];
 #pragma unroll
       for (int c = 0; c < 6; ++c) o[c] = (v[c] - mean) * rstd * gr[c] + be[c];
-      if constexpr (MOCR_STEM_LDS_OUT) {
-        float* os = xout[wave] + tw * 96 + c0;
+      float* os = xout[wave] + tw * 96 + c0;
 #pragma unroll
-        for (int e = 0; e < 3; ++e) *reinterpret_cast<float2*>(os + 2 * e) = make_float2(o[2 * e], o[2 * e + 1]);
-      } else if (tok < ntok) {
-        float* dst = X + (size_t)tok * 96 + c0;
-        *reinterpret_cast<float2*>(dst) = make_float2(o[0], o[1]);
-        *reinterpret_cast<float2*>(dst + 2) = make_float2(o[2], o[3]);
-        *reinterpret_cast<float2*>(dst + 4) = make_float2(o[4], o[5]);
-      }
+      for (int e = 0; e < 3; ++e) *reinterpret_cast<float2*>(os + 2 * e) = make_float2(o[2 * e], o[2 * e + 1]);
     }
-    if constexpr (MOCR_STEM_LDS_OUT) {  // the 16 tokens' 6 KB of X as whole 1 KB store instructions
+    {  // the 16 tokens' 6 KB of X as whole 1 KB store instructions
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -584,9 +508,8 @@ __device__ __forceinline__ floatx4 mfma3(const abf16x8& ah, const abf16x8& al, c
 // token's k / v then take the bias (selected, bitwise the old path's value) in the
 // windows that have one (a wave-uniform ballot).  The launcher splits the batch into
 // image chunks of < 2 GiB of QKV rows.
-#ifndef MOCR_WATT_STORE16  // 1: the O planes as 16-B stores, lane pairs trading halves (s4.wattn
-#define MOCR_WATT_STORE16 1  // 614 -> 558 us per 512 images, profiles/r05/r07x/); 0: 8-B stores
-#endif
+// the O planes as 16-B stores, lane pairs trading halves (s4.wattn 614 -> 558 us per 512
+// images against 8-B stores, profiles/r05/r07x/)
 template <int PASSES>
 __global__ void __launch_bounds__(256) window_attention_mfma_kernel(const float* __restrict__ QKV,
                                                                     const float* __restrict__ table, RowOut out,
@@ -752,7 +675,7 @@ __global__ void __launch_bounds__(256) window_attention_mfma_kernel(const float*
       floatx4 o = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 2; ++s) o = mfma3<PASSES>(vh[dt][s], vl[dt][s], ph[s], pl[s], o);
-      if (MOCR_WATT_STORE16 && !out.f32) {
+      if (!out.f32) {
         od[dt] = o;
         continue;
       }
@@ -768,7 +691,7 @@ __global__ void __launch_bounds__(256) window_attention_mfma_kernel(const float*
         }
       }
     }
-    if (MOCR_WATT_STORE16 && !out.f32 && out.hi && qr >= 0) {
+    if (!out.f32 && out.hi && qr >= 0) {
       // lanes g and g ^ 1 (16 apart, the same query row) trade halves: 8 consecutive
       // channels per lane, one 16-B store per plane (attend_to_planes in wattn.hip)
       const bool odd = g & 1;
@@ -875,19 +798,9 @@ void launch_stem(const float* img, const float* w, const float* b, const float* 
   // One resident round: 768 workgroups = 256 CUs x 3 waves per SIMD (150 VGPRs). 4096 paid
   // the weight prologue for 2-3 tokens per wave (profiles/r02/ab_stem_grid.log); 1024 left a
   // quarter-full second round: 829 -> 748 us per 512-image encode (profiles/r05/r07k/)
-#ifndef MOCR_STEM_BLOCKS
-#define MOCR_STEM_BLOCKS 768
-#endif
-#ifndef MOCR_STEM_WAVE16  // stem16w_kernel's prefetch depth in sweeps; 0 -> stem16_kernel
-#define MOCR_STEM_WAVE16 1
-#endif
-  if constexpr (MOCR_STEM_WAVE16 > 0) {
-    const unsigned blocks = (unsigned)std::min<long>((ntok + 63) / 64, MOCR_STEM_BLOCKS);
-    stem16w_kernel<MOCR_STEM_WAVE16><<<blocks, 256, 0, s>>>(img, w, b, ln_w, ln_b, X, ntok, H, W, Hs, Ws);
-  } else {
-    const unsigned blocks = (unsigned)std::min<long>((ntok + 15) / 16, MOCR_STEM_BLOCKS);
-    stem16_kernel<<<blocks, 256, 0, s>>>(img, w, b, ln_w, ln_b, X, ntok, H, W, Hs, Ws);
-  }
+  constexpr long kStemBlocks = 768;
+  const unsigned blocks = (unsigned)std::min<long>((ntok + 63) / 64, kStemBlocks);
+  stem16w_kernel<1><<<blocks, 256, 0, s>>>(img, w, b, ln_w, ln_b, X, ntok, H, W, Hs, Ws);  // one sweep ahead
   MOCR_HIP_CHECK(hipGetLastError());
 }
 

@@ -57,14 +57,6 @@ __device__ __forceinline__ floatx4 mma(const bf16x8 (&a)[2], const bf16x8 (&b)[2
   return c;
 }
 
-// timing probes of swin_attn_kernel (tools/build_variant.sh DIR -DMOCR_WATTN_PROBE=N; wrong
-// results): 1 no X loads (LN of zeros), 2 no qkv MFMAs, 3 no attention (S, softmax, PV),
-// 4 no proj MFMAs, 5 no weight loads (qkv and proj fragments from registers), 6 weight
-// fragments loaded on even k-steps only (odd k-steps reuse them), 7 the bias + mask tile of
-// query tile 0 reused for tiles 1-3
-#ifndef MOCR_WATTN_PROBE
-#define MOCR_WATTN_PROBE 0
-#endif
 // WPB windows per workgroup, HEADS waves each: the waves of one head in the WPB windows
 // load the same weight fragments at the same point of the same instruction stream (the
 // block's barriers keep them in step), so the CU's L1 can serve the later ones.
@@ -125,7 +117,7 @@ __global__ void __launch_bounds__(2 * C * WPB) __attribute__((amdgpu_waves_per_e
       const float* src = p.X + (size_t)(px[ps] < 0 ? 0 : px[ps]) * C + c0;  // clamped, masked below
 #pragma unroll
       for (int e = 0; e < 3; ++e) {
-        const floatx4 t = MOCR_WATTN_PROBE == 1 ? floatx4{1.f, 2.f, 3.f, 4.f} : *reinterpret_cast<const floatx4*>(src + 4 * e);
+        const floatx4 t = *reinterpret_cast<const floatx4*>(src + 4 * e);
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[ps][4 * e + k] = t[k];
       }
@@ -197,8 +189,7 @@ __global__ void __launch_bounds__(2 * C * WPB) __attribute__((amdgpu_waves_per_e
   auto wload = [&](int row0, int ks, bf16x8(&w)[2][2]) {
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
-      if constexpr (MOCR_WATTN_PROBE == 5) w[f][0] = w[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)ks, 1u, 2u, 3u});
-      else if (MOCR_WATTN_PROBE != 6 || (ks & 1) == 0) wfm(row0, f, ks, w[f]);
+      wfm(row0, f, ks, w[f]);
     }
   };
   // PRE: the double buffer (the k^T GEMM; the q^T GEMM runs with k and v live and keeps
@@ -221,7 +212,7 @@ __global__ void __launch_bounds__(2 * C * WPB) __attribute__((amdgpu_waves_per_e
         xfrag(ks, t, xf);
 #pragma unroll
         for (int f = 0; f < 2; ++f)
-          acc[f][t] = MOCR_WATTN_PROBE == 2 ? acc[f][t] + xf[0][0] : mma<X3>(w[ks & (PRE ? 1 : 0)][f], xf, acc[f][t]);
+          acc[f][t] = mma<X3>(w[ks & (PRE ? 1 : 0)][f], xf, acc[f][t]);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -261,7 +252,7 @@ __global__ void __launch_bounds__(2 * C * WPB) __attribute__((amdgpu_waves_per_e
         xfrag(ks, t, xf);
 #pragma unroll
         for (int f = 0; f < 2; ++f)
-          acc[t][f] = MOCR_WATTN_PROBE == 2 ? acc[t][f] + xf[0][0] : mma<X3>(xf, w[ks & 1][f], acc[t][f]);
+          acc[t][f] = mma<X3>(xf, w[ks & 1][f], acc[t][f]);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -314,17 +305,11 @@ __global__ void __launch_bounds__(2 * C * WPB) __attribute__((amdgpu_waves_per_e
   bm3 = tb[j16 * 64 + 48 + 4 * g];
 #pragma unroll
   for (int qt = 0; qt < 4; ++qt) {
-    if (qt > 0 && MOCR_WATTN_PROBE != 7) {
+    if (qt > 0) {
 #pragma unroll
       for (int kt = 0; kt < 3; ++kt)
         bm[kt] = *reinterpret_cast<const floatx4*>(tb + (16 * qt + j16) * 64 + 16 * kt + 4 * g);
       bm3 = tb[(16 * qt + j16) * 64 + 48 + 4 * g];
-    }
-    if constexpr (MOCR_WATTN_PROBE == 3) {
-      const int off = ((qt * HEADS + h) * 64 + lane) * 16;
-      *reinterpret_cast<bf16x8*>(lds + off) = kf[qt][0];
-      if constexpr (X3) *reinterpret_cast<bf16x8*>(lds + XB + off) = qf4[qt][1];
-      continue;
     }
     floatx4 st[4];
 #pragma unroll
@@ -409,12 +394,9 @@ __global__ void __launch_bounds__(2 * C * WPB) __attribute__((amdgpu_waves_per_e
   auto pload = [&](int hh, bf16x8(&wa)[2][2]) {
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
-      if constexpr (MOCR_WATTN_PROBE == 5) wa[f][0] = wa[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)hh, 1u, 2u, 3u});
-      else if (MOCR_WATTN_PROBE != 6 || (hh & 1) == 0) {
-        const int o = ((2 * h + f) * HEADS + hh) * 64 + lane;
-        wa[f][0] = wph[o];
-        if constexpr (X3) wa[f][1] = wpl[o];
-      }
+      const int o = ((2 * h + f) * HEADS + hh) * 64 + lane;
+      wa[f][0] = wph[o];
+      if constexpr (X3) wa[f][1] = wpl[o];
     }
   };
   bf16x8 wa[2][2][2];
@@ -431,7 +413,7 @@ __global__ void __launch_bounds__(2 * C * WPB) __attribute__((amdgpu_waves_per_e
       if constexpr (X3) of[1] = *reinterpret_cast<const bf16x8*>(lds + XB + off);
 #pragma unroll
       for (int f = 0; f < 2; ++f)
-        ap[f][t] = MOCR_WATTN_PROBE == 4 ? ap[f][t] + of[0][0] : mma<X3>(wa[hh & 1][f], of, ap[f][t]);
+        ap[f][t] = mma<X3>(wa[hh & 1][f], of, ap[f][t]);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -456,9 +438,7 @@ __global__ void __launch_bounds__(2 * C * WPB) __attribute__((amdgpu_waves_per_e
 // C of the no-proj kernels: attention of one head (K, V^T, Q^T fragments as B leaves
 // them) per 16-query tile; O goes to the ATT planes [window token row, C] at channels
 // ch0 + {4g.., 16+4g..} (tok0 = the window's first row)
-#ifndef MOCR_ATT_STORE16  // A/B builds: 1 -> the ATT planes as 16-B stores (lane pairs trade
-#define MOCR_ATT_STORE16 0   // halves): 12 B of scratch at C = 384, s3.attn 1 % slower (r05/r07t)
-#endif
+// (16-B stores with lane pairs trading halves measured 1 % slower at C = 384: r05/r07t)
 template <bool X3, int C>
 __device__ __forceinline__ void attend_to_planes(const bf16x8 (&kf)[4][2], const bf16x8 (&vf)[2][2][2],
                                                  const bf16x8 (&qf4)[4][2], const float* tb, int j16, int g,
@@ -521,28 +501,7 @@ __device__ __forceinline__ void attend_to_planes(const bf16x8 (&kf)[4][2], const
     }
     // ATT planes [row, C]: query token 16qt + j16 -> row orow[qt] (-1: not written),
     // channels 32h + {4g.., 16+4g..}
-    if (MOCR_ATT_STORE16 && orow[qt] >= 0) {
-      // lanes g and g ^ 1 (16 apart, the same query row) trade halves so that each holds 8
-      // consecutive channels: even g the dt = 0 run 4g .. 4g + 7, odd g the dt = 1 run
-      // 16 + 4(g - 1) .. 16 + 4g + 3; one 16-B store per plane instead of two 8-B ones
-      const bool odd = g & 1;
-      const size_t off = (size_t)orow[qt] * C + ch0 + (odd ? 16 + 4 * (g - 1) : 4 * g);
-#pragma unroll
-      for (int plane = 0; plane < (X3 ? 2 : 1); ++plane) {  // one plane at a time (registers)
-        uint32_t v[2][2], t;
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            if (plane) split2_bf16(x[4 * dt + 2 * e], x[4 * dt + 2 * e + 1], t, v[dt][e]);
-            else split2_bf16(x[4 * dt + 2 * e], x[4 * dt + 2 * e + 1], v[dt][e], t);
-          }
-        const uint32_t r0 = __shfl_xor(odd ? v[0][0] : v[1][0], 16);
-        const uint32_t r1 = __shfl_xor(odd ? v[0][1] : v[1][1], 16);
-        *reinterpret_cast<uint4*>((plane ? att_lo : att_hi) + off) =
-            odd ? make_uint4(r0, r1, v[1][0], v[1][1]) : make_uint4(v[0][0], v[0][1], r0, r1);
-      }
-    } else if (orow[qt] >= 0) {
+    if (orow[qt] >= 0) {
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
         const size_t off = (size_t)orow[qt] * C + ch0 + 16 * dt + 4 * g;
@@ -607,7 +566,7 @@ swin_attn_noproj_kernel(SwinAttnParams p) {
       const float* src = p.X + (size_t)(px[ps] < 0 ? 0 : px[ps]) * C + c0;  // clamped, masked below
 #pragma unroll
       for (int e = 0; e < 3; ++e) {
-        const floatx4 t = MOCR_WATTN_PROBE == 1 ? floatx4{1.f, 2.f, 3.f, 4.f} : *reinterpret_cast<const floatx4*>(src + 4 * e);
+        const floatx4 t = *reinterpret_cast<const floatx4*>(src + 4 * e);
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[ps][4 * e + k] = t[k];
       }
@@ -677,8 +636,7 @@ swin_attn_noproj_kernel(SwinAttnParams p) {
   auto wload = [&](int row0, int ks, bf16x8(&w)[2][2]) {
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
-      if constexpr (MOCR_WATTN_PROBE == 5) w[f][0] = w[f][1] = __builtin_bit_cast(bf16x8, uint4{(uint32_t)ks, 1u, 2u, 3u});
-      else if (MOCR_WATTN_PROBE != 6 || (ks & 1) == 0) wfm(row0, f, ks, w[f]);
+      wfm(row0, f, ks, w[f]);
     }
   };
   // acc[f][t] = W[row0 + 16f + j16, :] . LN^T (features x tokens)
@@ -698,7 +656,7 @@ swin_attn_noproj_kernel(SwinAttnParams p) {
         xfrag(ks, t, xf);
 #pragma unroll
         for (int f = 0; f < 2; ++f)
-          acc[f][t] = MOCR_WATTN_PROBE == 2 ? acc[f][t] + xf[0][0] : mma<X3>(w[ks & 1][f], xf, acc[f][t]);
+          acc[f][t] = mma<X3>(w[ks & 1][f], xf, acc[f][t]);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -1021,18 +979,13 @@ void launch_c(const SwinAttnParams& p, hipStream_t s) {
   else
     swin_attn_kernel<C, 1, OCC, WPB><<<grid, 2 * C * WPB, 0, s>>>(p);
 }
-// windows per workgroup (A/B builds: tools/build_variant.sh DIR -DMOCR_S1_WPB=2); at C = 192
+// windows per workgroup; at C = 192
 // two windows need 3 waves per SIMD (12 waves per workgroup).  Measured per 512-image encode
 // (two launches, profiles/r05/r06f/ops_*.log): C = 192 3.83-3.86 ms at two windows vs
 // 4.77 at one (590 KB of W_qkv + W_proj per window, read once per window pair from L2 /
 // L1); C = 96 6.86-6.90 ms at two vs 4.79 at one (147 KB per window; four 3-wave
 // workgroups per CU overlap better than two 6-wave ones)
-#ifndef MOCR_S1_WPB
-#define MOCR_S1_WPB 1
-#endif
-#ifndef MOCR_S2_WPB
-#define MOCR_S2_WPB 2
-#endif
+constexpr int kS1Wpb = 1, kS2Wpb = 2;
 
 // waves per SIMD the register allocation targets: 3 at C = 96 (534 vs 651 us per s1
 // block, 19 dwords spilled), 2 at C = 192 (509 vs 649 us: 94 spilled at 3).
@@ -1050,8 +1003,8 @@ void launch_swin_attn_fused(const SwinAttnParams& p, hipStream_t s) {
     throw std::runtime_error("swin_attn: fragment-major weights (launch_frag_pack) missing");
   if (p.heads * 32 != p.C) throw std::runtime_error("swin_attn: head dim must be 32");
   switch (p.C) {
-    case 96: launch_c<96, 3, MOCR_S1_WPB>(p, s); break;
-    case 192: launch_c<192, MOCR_S2_WPB == 1 ? 2 : 3, MOCR_S2_WPB>(p, s); break;
+    case 96: launch_c<96, 3, kS1Wpb>(p, s); break;
+    case 192: launch_c<192, kS2Wpb == 1 ? 2 : 3, kS2Wpb>(p, s); break;
     default: throw std::runtime_error("swin_attn: fused attention built for C = 96, 192");
   }
   MOCR_HIP_CHECK(hipGetLastError());

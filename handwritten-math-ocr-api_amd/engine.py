@@ -45,8 +45,11 @@ class KernelStat(ctypes.Structure):
 _lib = None
 
 
-def load_library(path: str = LIB_PATH):
-    """Load libmathocr.so once.  Raises if it has not been built (no silent fallback)."""
+def load_library(path: str = LIB_PATH, ab_build: bool = False):
+    """Load libmathocr.so once.  Raises if it has not been built (no silent fallback), if
+    it was built from other sources, or if it is not a production build (its baked
+    ``mocr_build_tag`` is not "production": compile-time definitions or a tools/ A/B build)
+    unless ``ab_build`` (the probes' and bench's ``--lib``, which report the tag)."""
     global _lib
     if _lib is not None:
         return _lib
@@ -55,6 +58,12 @@ def load_library(path: str = LIB_PATH):
     lib = ctypes.CDLL(path)
     lib.mocr_source_hash.restype = ctypes.c_char_p
     lib.mocr_source_hash.argtypes = []
+    lib.mocr_build_tag.restype = ctypes.c_char_p
+    lib.mocr_build_tag.argtypes = []
+    tag = lib.mocr_build_tag().decode()
+    if tag != "production" and not ab_build:
+        raise RuntimeError(f"{path} is not a production build (build tag {tag!r}): rebuild it with "
+                           f"`python -c 'import __graft_entry__ as g; g.build()'`, or load it as an A/B build")
     want = source_hash()
     if want is not None and lib.mocr_source_hash().decode() != want:
         raise RuntimeError(f"{path} was built from other sources (hash {lib.mocr_source_hash().decode()}, "
@@ -120,7 +129,7 @@ def source_hash():
 
 
 def exported_symbols():
-    return ["mocr_abi_version", "mocr_source_hash", "mocr_device_count", "mocr_weight_count", "mocr_memory_tokens", "mocr_create", "mocr_destroy",
+    return ["mocr_abi_version", "mocr_source_hash", "mocr_build_tag", "mocr_device_count", "mocr_weight_count", "mocr_memory_tokens", "mocr_create", "mocr_destroy",
             "mocr_last_error", "mocr_load_weights", "mocr_set_images", "mocr_set_images_device", "mocr_encode",
             "mocr_get_memory", "mocr_decode", "mocr_decode_device", "mocr_decode_beam", "mocr_debug_encode_until",
             "mocr_set_timing", "mocr_get_timing", "mocr_set_encoder_pos", "mocr_set_cu_mask", "mocr_set_stream_priority", "mocr_group_unique_id", "mocr_group_create",

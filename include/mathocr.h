@@ -133,6 +133,12 @@ int mocr_abi_version(void);
  * changed. */
 const char* mocr_source_hash(void);
 
+/* "production", or what made a non-production build: "defs:" and the compile-time
+ * definitions of a Makefile MOCR_DEFS build (e.g. the phase-clock -DMOCR_FOLD_TS), "ab:" and
+ * the tools/ script of an A/B build.  The Python binding refuses a non-production library
+ * unless it is loaded as an A/B build (the bench's --lib, which reports the tag). */
+const char* mocr_build_tag(void);
+
 /* HIP devices visible to the process (serving /health "device_available"); negative on a
  * HIP error, message in mocr_last_error(NULL). */
 int mocr_device_count(void);

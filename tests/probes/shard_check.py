@@ -17,7 +17,7 @@ ap.add_argument("--precision", default="bf16x3")
 a = ap.parse_args()
 pkg = importlib.import_module("handwritten-math-ocr-api_amd")
 if a.lib:
-    pkg.engine.load_library(a.lib)
+    pkg.engine.load_library(a.lib, ab_build=True)
 from tests.conftest import load_golden  # noqa: E402
 from oracle.gen_golden import apply_eos_boost  # noqa: E402
 

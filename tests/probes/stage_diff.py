@@ -11,7 +11,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402,F401
 
 pkg = importlib.import_module("handwritten-math-ocr-api_amd")
-pkg.engine.load_library(sys.argv[1])
+pkg.engine.load_library(sys.argv[1], ab_build=True)
 w = pkg.synth.make_weights(5, "perturbed")
 img = pkg.synth.make_images(1, 96, 320, 1000, "ink")
 out = {}

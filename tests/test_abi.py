@@ -62,3 +62,29 @@ def test_bad_config_rejected(pkg):
 def test_engine_fails_loudly_without_gpu(pkg):
     with pytest.raises(pkg.MocrError):
         pkg.Engine(img_hw=(96, 320), max_batch=1)
+
+
+def test_production_build_tag(pkg):
+    """the library bakes its build tag beside the source hash; the
+    in-tree library is a production build (no compile-time definitions)."""
+    lib = pkg.load_library()
+    assert lib.mocr_build_tag().decode() == "production"
+
+
+def test_non_production_build_is_refused(pkg, tmp_path, monkeypatch):
+    """A library built with compile-time definitions (Makefile MOCR_DEFS) or by a tools/
+    A/B script cannot load as the production library; the bench's --lib loads it as an A/B
+    build and reports the tag."""
+    import subprocess
+    src = tmp_path / "fake.c"
+    src.write_text('const char* mocr_source_hash(void) { return "x"; }\n'
+                   'const char* mocr_build_tag(void) { return "defs:-DMOCR_FOLD_TS"; }\n')
+    so = tmp_path / "libfake.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", str(src), "-o", str(so)], check=True)
+    monkeypatch.setattr(pkg.engine, "_lib", None)
+    with pytest.raises(RuntimeError, match="not a production build"):
+        pkg.engine.load_library(str(so))
+    # as an A/B build it passes the tag check and stops at the source hash
+    with pytest.raises(RuntimeError, match="other sources"):
+        pkg.engine.load_library(str(so), ab_build=True)
+    monkeypatch.setattr(pkg.engine, "_lib", None)

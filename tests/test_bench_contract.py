@@ -209,3 +209,52 @@ def test_rank0_stdout_is_one_json_line_with_gloo(tmp_path):
     lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, out.stdout
     assert json.loads(lines[0]) == {"metric": "x", "n": 2}
+
+
+def test_serving_latency_is_the_reference_serving_call(bench):
+    """serving_latency_ms times im2latex.predict on one 96x320 image
+    (batch stop, 150-step cap) and a fixed 128-step decode, median of >= 10 calls."""
+    import types
+    calls = {"predict": 0, "decode": []}
+
+    class Eng:
+        def __init__(self, img_hw, max_batch, precision, device):
+            assert img_hw == (96, 320) and max_batch == 1
+            self.closed = False
+
+        def load_weights(self, w):
+            pass
+
+        def encode(self, img):
+            assert img.shape == (1, 1, 96, 320)
+
+        def decode(self, max_steps, stop):
+            calls["decode"].append((max_steps, stop))
+            return types.SimpleNamespace(n_steps=max_steps if stop == "none" else 37)
+
+        def close(self):
+            self.closed = True
+
+    def predict(eng, img, vocab, idx2char):
+        calls["predict"] += 1
+        return ("x", 0.5)
+
+    import numpy as np
+    pkg = types.SimpleNamespace(
+        Engine=Eng, im2latex=types.SimpleNamespace(predict=predict),
+        synth=types.SimpleNamespace(synthetic_vocab=lambda: ({}, {}),
+                                    make_images=lambda n, h, w, seed0: np.zeros((n, 1, h, w), np.float32)),
+        config=types.SimpleNamespace(config=types.SimpleNamespace(max_seq_len=150)))
+    r = bench.serving_latency(pkg, {}, "bf16x3", 0)
+    assert r["samples"] >= 10 and calls["predict"] == r["samples"] + 2
+    assert r["fixed_steps"] == 128 and r["im2latex_predict_steps"] == 37
+    assert (150, "batch") in calls["decode"] and r["image"] == [96, 320] and r["batch"] == 1
+    assert r["im2latex_predict"] >= 0 and r["fixed_128_steps"] >= 0
+
+
+def test_latency_pass_has_at_least_16_samples():
+    """The headline p50 comes from >= 16 loaded calls run after the timed region."""
+    src = open(os.path.join(REPO, "bench.py")).read()
+    assert "lat_pass = run(max(16, 2 * R))" in src
+    assert '"p50_image_latency_ms": statistics.median(lat_pass) * 1e3' in src
+    assert '"image_latency_samples": len(lat_pass)' in src

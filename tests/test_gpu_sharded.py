@@ -192,8 +192,9 @@ def test_bench_two_ranks_torchrun():
     assert len(lines) == 1, r.stdout[-2000:]
     out = json.loads(lines[0])
     cfg = out["config"]
-    assert out["n_gpus"] == 2 and out["value"] > 0 and cfg["global_batch"] == 2 * cfg["images_per_call"]
-    assert cfg["images_per_call"] == cfg["per_gpu_batch"] == cfg["batch_unit"] * cfg["batches_per_chain"]
+    assert out["n_gpus"] == 2 and out["value"] > 0 and cfg["global_batch"] == 2 * cfg["per_gpu_batch"]
+    assert cfg["per_gpu_batch"] == cfg["batch_unit"] == 64
+    assert cfg["images_per_call"] == cfg["batch_unit"] * cfg["batches_per_chain"]
     assert len(out["rank_elapsed_s"]["all"]) == 2 and out["rank_elapsed_s"]["max"] * 1e3 / out["steps"] == \
         pytest.approx(out["ms_per_step"])
     assert out["config"]["gather"] in ("rccl (mocr_group_gather_ids)", "gloo host (ranks share a device)")

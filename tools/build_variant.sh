@@ -12,7 +12,7 @@ done
 wait
 # the source hash the Makefile bakes in (engine.load_library checks it)
 H=$(cat $(ls csrc/*.hip csrc/*.h | LC_ALL=C sort) ../include/mathocr.h | sha256sum | cut -c1-16)
-printf 'extern "C" const char* mocr_source_hash(void) { return "%s"; }\n' $H > "$OUT/obj/srchash.cpp"
+printf 'extern "C" const char* mocr_source_hash(void) { return "%s"; }\nextern "C" const char* mocr_build_tag(void) { return "ab:%s"; }\n' $H "build_variant.sh $*" > "$OUT/obj/srchash.cpp"
 g++ -O2 -fPIC -c "$OUT/obj/srchash.cpp" -o "$OUT/obj/srchash.o"
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$OUT/libmathocr.so" "$OUT"/obj/*.o -ldl
 echo "built $OUT/libmathocr.so"

@@ -30,7 +30,7 @@ ap.add_argument("--variant", default="", help="comma-separated engine.VARIANT na
 a = ap.parse_args()
 pkg = importlib.import_module("handwritten-math-ocr-api_amd")
 if a.lib:
-    pkg.engine.load_library(a.lib)
+    pkg.engine.load_library(a.lib, ab_build=True)
 w = pkg.synth.make_weights(1234, "init")
 S = a.steps
 out = []

@@ -21,7 +21,7 @@ ap.add_argument("--decode", type=int, default=0, help="also decode this many gre
 a = ap.parse_args()
 pkg = importlib.import_module("handwritten-math-ocr-api_amd")
 if a.lib:
-    pkg.engine.load_library(a.lib)
+    pkg.engine.load_library(a.lib, ab_build=True)
 var = tuple(v for v in a.variant.split(",") if v)
 eng = pkg.Engine(img_hw=(384, 384), max_batch=a.batch, precision="bf16x3", variant=var)
 eng.load_weights(pkg.synth.make_weights(1234, "init"))

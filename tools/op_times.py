@@ -20,7 +20,7 @@ ap.add_argument("--batch", type=int, default=64)
 a = ap.parse_args()
 pkg = importlib.import_module("handwritten-math-ocr-api_amd")
 if a.lib:
-    pkg.engine.load_library(a.lib)
+    pkg.engine.load_library(a.lib, ab_build=True)
 imgs = pkg.synth.make_images(a.batch, 384, 384)
 w = pkg.synth.make_weights(1234, "init")
 res = {}

@@ -23,7 +23,7 @@ ap.add_argument("--rows", type=int, default=64, help="images per engine call (de
 a = ap.parse_args()
 pkg = importlib.import_module("handwritten-math-ocr-api_amd")
 if a.lib:
-    pkg.engine.load_library(a.lib)
+    pkg.engine.load_library(a.lib, ab_build=True)
 B, S = a.rows, 128
 pool = pkg.pipeline.ReplicaPool(a.replicas, img_hw=(384, 384), max_batch=B, precision=a.precision, device=0)
 pool.load_weights(pkg.synth.make_weights(1234, "init"))

@@ -3,7 +3,7 @@
 # the micro-batched /predict and the uneven-shard gather; smoke; the bench in both forms.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-O=gpurun_out/s6c; mkdir -p $O
+O=gpurun_out/${TAG:-s6c}; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread \
   > $O/tests.log 2>&1 || { echo "TESTS FAILED"; grep -E 'FAILED|Error|error' $O/tests.log | head -20; tail -40 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
@@ -13,5 +13,6 @@ timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > $O/bench_driver.jso
 python -c "
 import json; d=json.load(open('$O/bench_driver.json')); k=d['kernel_classes']
 print('driver', d['value'], d['ms_per_step'], 'dec', d['roofline']['avg_step_ms'], 'gemm', d['roofline_gemm']['kernel'], d['roofline_gemm']['frac'])
-print({c: round(v['avg_ms']*v['launches']/3, 3) for c, v in k.items() if c.startswith('s3')})"
+print({c: round(v['avg_ms']*v['launches']/3, 3) for c, v in k.items() if c.startswith('s3')})
+print('p50', d['p50_image_latency_ms'], d['image_latency_samples'], 'serving', d.get('serving_latency_ms'), 'build', d['config']['build'])"
 echo done

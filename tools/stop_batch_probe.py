@@ -26,7 +26,7 @@ ap.add_argument("--eos-boost", default="0")
 a = ap.parse_args()
 pkg = importlib.import_module("handwritten-math-ocr-api_amd")
 if a.lib:
-    pkg.engine.load_library(a.lib)
+    pkg.engine.load_library(a.lib, ab_build=True)
 out = {"lib": a.lib or "default"}
 for boost in [float(x) for x in a.eos_boost.split(",")]:
     w = pkg.synth.make_weights(1234, "init")
