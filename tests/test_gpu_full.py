@@ -220,18 +220,18 @@ def test_config4_beam4_b32_256(pkg, golden):
     np.testing.assert_allclose(res.scores[:2], g["scores"], rtol=1e-5, atol=1e-3)
     assert (np.diff(res.scores, axis=1) <= 0).all()
     # beam = 1 is greedy decoding, over all 32 rows and 256 steps.  Since round 5 both run
-    # the same folded kernels (beam: over its hypotheses' slot tables), so the logits are the
-    # same and only the selection differs (beam: the top-1 of the fp32 log-softmax, ties to
-    # the lower index; greedy: the first argmax of the logits): a row can part only where
-    # two logits are within a log-softmax rounding (~1e-6) of each other.  Every row without
-    # such a step is compared in full (was rows without a 1e-4 near-tie).
+    # the folded layer kernels (beam over its hypotheses' slot tables), but the two steps are
+    # not the same bits end to end: round 6 tried a 1e-6 near-tie threshold and row 13 parted
+    # at a step whose top-2 margin lies between 1e-6 and 1e-4 (profiles/r06/s6d/tests.log).
+    # So every row is compared up to its first step with a margin below 1e-4, and the rows
+    # without one (24 of 32) in full (the old bound only asked for 16 of them).
     b1 = eng.beam_search(beam=1, max_steps=S, stop="none")
     gr = eng.decode(max_steps=S, stop="none", want_logits=True)
     top2 = np.sort(gr.logits, -1)[..., -2:]
     margins = top2[..., 1] - top2[..., 0]
     rec = {"config": "C4 beam 1 vs greedy, B=32, 256 steps"}
-    n_full = check_ids(b1.ids, gr.ids, margins, tie=1e-6, record=rec)
-    assert n_full == int((margins >= 1e-6).all(axis=1).sum()), rec
+    n_full = check_ids(b1.ids, gr.ids, margins, tie=1e-4, record=rec)
+    assert n_full == int((margins >= 1e-4).all(axis=1).sum()) >= 24, rec
     again = eng.beam_search(beam=K, max_steps=S, stop="none")
     np.testing.assert_array_equal(again.beams, res.beams)
     eng.close()
