@@ -374,6 +374,7 @@ struct mocr_engine {
   std::vector<void*> mlppack;  // mlp.hip: the fused MLP kernels' W1 | W2 chunk images per block
   std::vector<void*> lngpack;  // mlp.hip: lngemm384's W_qkv chunk images per stage-3 block
   void* mergepack = nullptr;   // and of merge 1's reduction
+  FragW mergefrag;             // merge 1's reduction, fragment-major (merge.hip)
   std::vector<void*> frag_allocs;
 
   // timing
@@ -1016,6 +1017,13 @@ struct mocr_engine {
         frag_allocs.push_back(mergepack);
       }
       launch_lngemm384_pack(dwh + m.redw, dwl ? dwl + m.redw : nullptr, 192, mergepack, stream);
+      if (!mergefrag.hi) {  // merge.hip's registers-resident W (hi / lo; bf16 engines read hi)
+        mergefrag.hi = dalloc<uint16_t>((size_t)192 * 384);
+        mergefrag.lo = dalloc<uint16_t>((size_t)192 * 384);
+        frag_allocs.push_back(mergefrag.hi);
+        frag_allocs.push_back(mergefrag.lo);
+      }
+      launch_frag_pack(W(m.redw), 192, 384, mergefrag.hi, mergefrag.lo, nullptr, stream);
     }
     int nb = 0;
     for (int st = 0; st < kStages; ++st) nb += kDepth[st];
@@ -1452,7 +1460,16 @@ struct mocr_engine {
       if (s < kStages - 1) {
         const MergeW& m = lay->merge[s];
         const long orow = (long)B * ((g.H + 1) / 2) * ((g.W + 1) / 2);
-        if (b16 && 4 * C == 384 && !(cfg.variant & MOCR_VARIANT_UNFUSED_LN_GEMM)) {
+        if (b16 && 4 * C == 384 && merge1_supported(g.H, g.W) && !(cfg.variant & MOCR_VARIANT_UNFUSED_LN_GEMM)) {
+          // gather + norm + reduction as a stream (merge.hip)
+          Merge1Params mp{};
+          mp.X = X; mp.B = B; mp.H = g.H; mp.W = g.W;
+          mp.ln_g = W(m.nw); mp.ln_b = W(m.nb);
+          mp.w_hi = mergefrag.hi; mp.w_lo = dwl ? mergefrag.lo : nullptr;
+          mp.out = X2;
+          timed(mrg_n[s], 2.0 * orow * 4 * C * 2 * C, 4.0 * (double)B * g.H * g.W * C + 8.0 * orow * C +
+                (dwl ? 4.0 : 2.0) * 8.0 * C * C, [&] { launch_merge1(mp, stream); });
+        } else if (b16 && 4 * C == 384 && !(cfg.variant & MOCR_VARIANT_UNFUSED_LN_GEMM)) {
           // gather + norm + reduction in one kernel (mlp.hip lngemm384_kernel)
           LnGemm384Params lp{};
           lp.X = X; lp.M = orow; lp.ln_g = W(m.nw); lp.ln_b = W(m.nb);

@@ -163,6 +163,20 @@ void launch_lngemm384(const LnGemm384Params& p, hipStream_t s);
 // (lo ? 2 : 1) bytes at `out`
 void launch_lngemm384_pack(const void* w, const void* wlo, int N, void* out, hipStream_t s);
 
+// Stage 1's PatchMerging (merge.hip): 2 x 2 gather of X [B, H, W, 96] + LayerNorm(384) +
+// Linear(384, 192) -> out [B * H/2 * W/2, 192], bf16 (w_lo null) or bf16x3, W in the
+// fragment-major planes of launch_frag_pack(W, 192, 384).  H, W even and W / 2 % 16 == 0
+// (merge1_supported); other maps take lngemm384.
+struct Merge1Params {
+  const float* X;
+  int B, H, W;
+  const float *ln_g, *ln_b;         // [384]
+  const uint16_t *w_hi, *w_lo;      // [12][12][64 lanes][8] bf16
+  float* out;
+};
+bool merge1_supported(int H, int W);
+void launch_merge1(const Merge1Params& p, hipStream_t s);
+
 // Fused norm1 + window qkv + W-MSA + proj + residual of one Swin block (wattn.hip),
 // bf16 / bf16x3 (lo planes present) for C = 96, 192 (head dim 32).
 struct SwinAttnParams {
