@@ -497,12 +497,6 @@ __device__ __forceinline__ void wide_tile(const FoldGemmParams& p, int r0, int c
   MOCR_TS(6, __builtin_amdgcn_s_memrealtime());
 }
 
-#ifndef MOCR_FOLD_XCD_COLS
-#define MOCR_FOLD_XCD_COLS 0
-#endif
-constexpr int XC = MOCR_FOLD_XCD_COLS;
-static_assert(XC == 0 || XC == 1 || XC == 2 || XC == 4 || XC == 8, "column groups divide ncol (a multiple of 8)");
-
 template <int BM, int BN, int K1, bool S1, bool S2, bool X3, bool LOGITS, int NW, int PD>
 __global__ void __launch_bounds__(64 * NW) foldwide_kernel(FoldGemmParams p) {
   constexpr int BYTES = LOGITS ? TileLds<BM, BN, false, 0, X3, NW>::BYTES
@@ -512,26 +506,8 @@ __global__ void __launch_bounds__(64 * NW) foldwide_kernel(FoldGemmParams p) {
   __shared__ __attribute__((aligned(16))) char smem[BYTES];
   const int ncol = (p.NY + p.NZ) / BN;
   const int b = blockIdx.x;
-  int c0, r0;
-  if constexpr (XC > 0 && !LOGITS) {
-    // XCD-local tiles: blocks b, b + 8, ... share an XCD (round-robin placement, speed only).
-    // The tiles are ordered column group cg = col % XC first, then row, then col / XC, and
-    // cut into 8 equal chunks; the blocks of one XCD take one chunk.  So an XCD works on
-    // 1/XC of the columns (y and z tiles interleaved) and 8/XC-th of the rows: A rows reach
-    // XC of the 8 L2s and each weight column tile 8 / XC of them, instead of every A row
-    // reaching all 8 (column tile = b % ncol).  ncol % 8 == 0, so 8 divides the tile count.
-    const int nrow = (p.B + BM - 1) / BM;
-    const int per = nrow * ncol / 8;
-    const int pos = (b % 8) * per + b / 8;
-    const int ncg = ncol / (XC > 0 ? XC : 1);
-    const int cg = pos / (nrow * ncg);
-    const int rem = pos - cg * (nrow * ncg);
-    r0 = (rem / ncg) * BM;
-    c0 = ((rem % ncg) * (XC > 0 ? XC : 1) + cg) * BN;
-  } else {
-    c0 = (b % ncol) * BN;
-    r0 = (b / ncol) * BM;
-  }
+  const int c0 = (b % ncol) * BN;
+  const int r0 = (b / ncol) * BM;
   if constexpr (LOGITS) {
     wide_tile<BM, BN, false, 0, false, true, X3, true, NW, PD>(p, r0, c0, smem);
   } else {
