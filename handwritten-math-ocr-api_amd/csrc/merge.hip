@@ -17,8 +17,9 @@
 //    the whole kernel: wave w owns output channels 48 w .. 48 w + 47 (3 tiles of 16), 72
 //    A fragments; out^T [48 x 16] = W_w . LN^T, three MFMAs per product in bf16x3;
 //  - each lane stores 4 consecutive channels of one row per output tile (16-B stores).
-// Two raw barriers per tile (LN reads the landed tile / the MFMAs read the fragments); the
-// DMA waits count this wave's own vector-memory operations (see the loop).
+// A software pipeline with one raw barrier per tile: tile i's MFMAs beside tile i+1's
+// LayerNorm (double-buffered fragments); the DMA waits count this wave's own vector-memory
+// operations (see the loop).
 #include "kernels.h"
 #include "lanes.h"
 
@@ -65,7 +66,7 @@ template <int PASSES>
 __global__ void __launch_bounds__(256) merge1_kernel(Merge1Params p) {
   constexpr bool X3 = PASSES == 3;
   __shared__ __attribute__((aligned(16))) char raw[kRing][kRawBytes];
-  __shared__ __attribute__((aligned(16))) char frag[12 * 2 * 1024];  // [k-step][plane][lane] x 16 B
+  __shared__ __attribute__((aligned(16))) char frag[2][12 * 2 * 1024];  // [tile % 2][k-step][plane][lane] x 16 B
   __shared__ __attribute__((aligned(16))) float gam[kMK], bet[kMK];
 
   const int tid = threadIdx.x;
@@ -78,7 +79,8 @@ __global__ void __launch_bounds__(256) merge1_kernel(Merge1Params p) {
   if (my <= 0) return;
 
   // the DMA of local tile i (a tile past the end re-reads the first: the ring's wait counts
-  // stay those of the steady state; its slot is never read)
+  // stay those of the steady state, and the LayerNorm of "tile my" reads valid data; neither
+  // result is used)
   auto issue = [&](int i) __attribute__((always_inline)) {
     const int T = (int)blockIdx.x + (i < my ? i : 0) * G;
     const int b = T / (H2 * JT);
@@ -117,66 +119,72 @@ __global__ void __launch_bounds__(256) merge1_kernel(Merge1Params p) {
   const int row = tid >> 4;  // LayerNorm: tile row, and this lane's 24 channels
   const int l16 = tid & 15;
   const int j16 = lane & 15, g = lane >> 4;
-  for (int i = 0; i < my; ++i) {
-    // this wave's DMA of tile i landed: after it the wave issued (steady state) tile i-3's
-    // stores, tile i+1's DMA, tile i-2's stores, tile i+2's DMA, tile i-1's stores
-    if (i == 0)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kDmaPerWave) : "memory");
-    else if (i == 1)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kDmaPerWave + kStoresPerTile) : "memory");
-    else if (i == 2)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kDmaPerWave + 2 * kStoresPerTile) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kDmaPerWave + 3 * kStoresPerTile) : "memory");
-    __builtin_amdgcn_s_barrier();  // every wave's pieces landed; every wave is past tile i-1's MFMAs
-    // ---- LayerNorm of row `row`, channels 24 l16 .. + 23, into the B fragments
-    {
-      const float* xr = reinterpret_cast<const float*>(raw[i % kRing]) + row * kMK + 24 * l16;
-      float v[24];
+  // LayerNorm of tile i's row `row`, channels 24 l16 .. + 23, into B-fragment buffer i % 2
+  auto layernorm = [&](int i) __attribute__((always_inline)) {
+    const float* xr = reinterpret_cast<const float*>(raw[i % kRing]) + row * kMK + 24 * l16;
+    float v[24];
 #pragma unroll
-      for (int e = 0; e < 6; ++e) {
-        const floatx4 a = *reinterpret_cast<const floatx4*>(xr + 4 * e);
+    for (int e = 0; e < 6; ++e) {
+      const floatx4 a = *reinterpret_cast<const floatx4*>(xr + 4 * e);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[4 * e + r] = a[r];
-      }
-      float s = 0.f;
-#pragma unroll
-      for (int e = 0; e < 24; ++e) s += v[e];
-      const float mean = row_sum<16>(s) * (1.0f / kMK);
-      float q = 0.f;
-#pragma unroll
-      for (int e = 0; e < 24; ++e) {
-        const float d = v[e] - mean;
-        q += d * d;
-      }
-      const float rstd = 1.0f / sqrtf(row_sum<16>(q) * (1.0f / kMK) + 1e-5f);
-#pragma unroll
-      for (int h = 0; h < 3; ++h) {  // k8 group 3 l16 + h: k-step k8 / 4, lane group k8 % 4
-        const int k8 = 3 * l16 + h;
-        float y[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int k = 8 * k8 + e;
-          y[e] = (v[8 * h + e] - mean) * rstd * gam[k] + bet[k];
-        }
-        bf16x8 hi, lo;
-        split8(y, hi, lo);
-        const int fl = (k8 & 3) * 16 + row;  // fragment lane: lane group, row
-        char* fp = frag + ((k8 >> 2) * 2 * 64 + fl) * 16;
-        *reinterpret_cast<bf16x8*>(fp) = hi;
-        if constexpr (X3) *reinterpret_cast<bf16x8*>(fp + 1024) = lo;
-      }
+      for (int r = 0; r < 4; ++r) v[4 * e + r] = a[r];
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // the fragments are in LDS; tile i's raw slot is free
-    issue(i + kRing);
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < 24; ++e) s += v[e];
+    const float mean = row_sum<16>(s) * (1.0f / kMK);
+    float q = 0.f;
+#pragma unroll
+    for (int e = 0; e < 24; ++e) {
+      const float d = v[e] - mean;
+      q += d * d;
+    }
+    const float rstd = 1.0f / sqrtf(row_sum<16>(q) * (1.0f / kMK) + 1e-5f);
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {  // k8 group 3 l16 + h: k-step k8 / 4, lane group k8 % 4
+      const int k8 = 3 * l16 + h;
+      float y[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = 8 * k8 + e;
+        y[e] = (v[8 * h + e] - mean) * rstd * gam[k] + bet[k];
+      }
+      bf16x8 hi, lo;
+      split8(y, hi, lo);
+      const int fl = (k8 & 3) * 16 + row;  // fragment lane: lane group, row
+      char* fp = frag[i & 1] + ((k8 >> 2) * 2 * 64 + fl) * 16;
+      *reinterpret_cast<bf16x8*>(fp) = hi;
+      if constexpr (X3) *reinterpret_cast<bf16x8*>(fp + 1024) = lo;
+    }
+  };
+
+  // software pipeline, one barrier per tile: iteration i runs tile i's MFMAs (fragment
+  // buffer i % 2) beside tile i+1's LayerNorm (raw slot (i+1) % 3 -> buffer (i+1) % 2), so
+  // the LayerNorm's VALU work fills the MFMAs' issue gaps
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kDmaPerWave) : "memory");  // tile 0 landed (this wave's pieces)
+  __builtin_amdgcn_s_barrier();
+  layernorm(0);
+  for (int i = 0; i < my; ++i) {
+    // tile i+1's DMA landed: after it this wave issued tile i+2's DMA (iteration i-1, or the
+    // prologue) and tiles i-2's and i-1's stores
+    if (i == 0)
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kDmaPerWave) : "memory");
+    else if (i == 1)
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kDmaPerWave + kStoresPerTile) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kDmaPerWave + 2 * kStoresPerTile) : "memory");
+    // every wave: tile i's fragments written, tile i+1's pieces landed, tile i-1's MFMAs (the
+    // other fragment buffer) and tile i's LayerNorm (its raw slot) done
+    __builtin_amdgcn_s_barrier();
+    issue(i + kRing);  // into tile i's raw slot
     // ---- out^T [48 x 16] = W_w . LN^T over 12 k-steps (three passes per product in bf16x3)
     floatx4 acc[3];
 #pragma unroll
     for (int t = 0; t < 3; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const char* fb = frag[i & 1];
 #pragma unroll
     for (int ks = 0; ks < 12; ++ks) {
-      const char* fp = frag + (ks * 2 * 64 + lane) * 16;
+      const char* fp = fb + (ks * 2 * 64 + lane) * 16;
       const bf16x8 bh = *reinterpret_cast<const bf16x8*>(fp);
       bf16x8 bl;
       if constexpr (X3) bl = *reinterpret_cast<const bf16x8*>(fp + 1024);
@@ -189,6 +197,7 @@ __global__ void __launch_bounds__(256) merge1_kernel(Merge1Params p) {
         for (int t = 0; t < 3; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t][ks][1], bh, acc[t], 0, 0, 0);
       }
     }
+    layernorm(i + 1);  // independent of the MFMAs above: the scheduler interleaves them
     // lane (g, j16): output row j16, channels 16 (3 wave + t) + 4 g .. + 3
     {
       const int T = (int)blockIdx.x + i * G;
