@@ -4,7 +4,7 @@ A greedy decode step is a chain of small, latency-bound kernels, while the encod
 throughput-bound stream of large GEMMs.  Calls are independent, so R engines on the same
 device, each driven by its own thread (ctypes releases the GIL; each engine has its own
 HIP stream), overlap one call's decode with another call's encoder.  The GPU time of the
-two halves still adds up rather than hiding one behind the other (DESIGN.md §5.5-5.6,
+two halves still adds up rather than hiding one behind the other (DESIGN.md §5.5, docs/DESIGN_history_r01-r05.md §5.6;
 tools/pipeline_probe.py measures encode-only, decode-only and both).
 
 ``imap`` preserves submission order, so callers can run an order-sensitive step

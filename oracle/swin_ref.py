@@ -19,7 +19,7 @@ installed in this image, so this file restates its published algorithm
 Parity of this restatement is pinned against HF ``SwinModel`` at 384×384
 (``oracle/hf_crosscheck.py``).  The 96×320 padded/shift-disabled corner cases are
 not covered by any installed implementation ("parity unpinned" for those, see
-DESIGN.md §Oracle) and follow torchvision's ``shifted_window_attention`` exactly.
+DESIGN.md §4) and follow torchvision's ``shifted_window_attention`` exactly.
 """
 from __future__ import annotations
 

@@ -1,6 +1,6 @@
 """Decode-only throughput of R concurrent replicas, each on all CUs or on its own
 contiguous CU range (mocr_set_cu_mask), to test whether per-XCD isolation removes the
-replicas' mutual slowdown."""
+replicas' mutual slowdown (docs/DESIGN_history_r01-r05.md §5.6)."""
 import importlib
 import json
 import os
