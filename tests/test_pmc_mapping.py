@@ -96,3 +96,23 @@ def test_stage3_block_tail_maps_to_s3_tail(tmp_path):
     assert cls["s3.attn"]["launches"] == 6 and "noproj" in cls["s3.attn"]["kernel"]
     assert cls["s3.tail"]["launches"] == 6 and "mlp384_kernel<3, true" in cls["s3.tail"]["kernel"]
     assert "s3.proj" not in cls and "s3.mlp" not in cls and cls["merge1"]["launches"] == 1
+
+
+def test_round6_encode_merge1_kernel(tmp_path):
+    """Round 6 production at 640 images: merge 1 on the persistent merge1_kernel (merge.hip),
+    stage 3 as fused attention + block tail, so no lngemm384 dispatch remains."""
+    tool = load_tool()
+    k = bench_dispatches()
+    a = k.index("mocr::lngemm384_kernel<3, 2>", k.index("mocr::ln_group_kernel<64, 12, 2>"))
+    b = k.index("mocr::ln_group_kernel<64, 24, 2>")
+    names = k[:a] + ["mocr::swin_attn_noproj_kernel<384, 3, 3, 12, 2>", "mocr::mlp384_kernel<3, true, 4>"] * 6 + k[b:]
+    names = [("mocr::merge1_kernel<3>" if "lngemm384" in n else n) for n in names]
+    names = [("mocr::stem16w_kernel" if "stem" in n else n) for n in names]
+    assert not any("lngemm384" in n for n in names)
+    write_csv(tmp_path / "f.csv", names, 1.0)
+    write_csv(tmp_path / "w.csv", names, 1.0)
+    tool.main(str(tmp_path / "f.csv"), str(tmp_path / "w.csv"), str(tmp_path / "o.json"))
+    cls = json.load(open(tmp_path / "o.json"))["classes"]
+    assert cls["merge1"]["launches"] == 1 and "merge1_kernel" in cls["merge1"]["kernel"]
+    assert "merge1.ln" not in cls and cls["s3.tail"]["launches"] == 6
+    assert "ln_group_kernel<64, 12, 2>" in cls["merge2.ln"]["kernel"]

@@ -73,7 +73,9 @@ def main(fetch_csv, write_csv, out, decode_steps=0, batch=0):
     anoproj = [3] if any("swin_attn_noproj_kernel" in k for k in kn) else []
     n_lng = sum("lngemm384_kernel" in k for k in kn)  # 6 stage-3 blocks and / or merge 1
     lnqkv = [3] if n_lng >= 6 else []
-    lnmerge = [1] if n_lng in (1, 7) else []
+    # merge 1 as one dispatch: lngemm384 (rounds 4-5, and maps whose W/2 % 16 != 0) or the
+    # persistent merge1_kernel (merge.hip, round 6)
+    lnmerge = [1] if n_lng in (1, 7) or any("merge1_kernel" in k for k in kn) else []
     tail = [3] if any("mlp384_kernel<" in k and ", true" in k for k in kn) else []
     names = with_memkv24(classes_in_order(fused, afused, anoproj, lnqkv, lnmerge, tail), kn)
     # load-time bf16 splits before the stem: weights, kv-weights, and (bf16x3) the folded
