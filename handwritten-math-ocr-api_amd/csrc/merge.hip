@@ -9,7 +9,7 @@
 // Persistent workgroups (one per CU) loop over tiles of 16 output rows, i.e. 32 pixels
 // of two consecutive image rows, which are two contiguous 12 KB runs of X:
 //  - the tile's 24 KB reach LDS by LDS-DMA (global_load_lds, 16 B per lane) already in
-//    gathered order [row][384], three tiles ahead (no staging registers);
+//    gathered order [row][384], four tiles ahead (no staging registers);
 //  - LayerNorm: 16 lanes per row, 24 channels each, the sums over the row's 16 lanes on
 //    DPP; the normalised rows are split into bf16 hi / lo and written to LDS as the MFMA B
 //    fragments (k-step, plane, lane);
@@ -34,7 +34,7 @@ constexpr int kMK = 4 * kMC;      // LayerNorm / GEMM k
 constexpr int kMN = 2 * kMC;      // output channels
 constexpr int kMRows = 16;        // output rows per tile
 constexpr int kRawBytes = kMRows * kMK * 4;  // 24 KB: one tile, gathered, fp32
-constexpr int kRing = 3;          // tiles in flight
+constexpr int kRing = 4;          // tiles in flight (LDS: 4 x 24 KB raw + 2 x 24 KB fragments)
 constexpr int kDmaPerWave = kRawBytes / 1024 / 4;  // 1-KB pieces per wave and tile (6)
 constexpr int kStoresPerTile = 3; // 16-B stores per lane and tile (3 output tiles per wave)
 static_assert(kDmaPerWave * 4 * 1024 == kRawBytes, "four waves split the tile's pieces");
@@ -98,9 +98,8 @@ __global__ void __launch_bounds__(256) merge1_kernel(Merge1Params p) {
       dma16(img, (uint32_t)(((size_t)py * p.W + px) * kMC + c) * 4u, lds_u32(dst + piece * 1024));
     }
   };
-  issue(0);
-  issue(1);
-  issue(2);
+#pragma unroll
+  for (int i = 0; i < kRing; ++i) issue(i);
   for (int i = tid; i < kMK; i += 256) {
     gam[i] = p.ln_g[i];
     bet[i] = p.ln_b[i];
@@ -159,20 +158,24 @@ __global__ void __launch_bounds__(256) merge1_kernel(Merge1Params p) {
   };
 
   // software pipeline, one barrier per tile: iteration i runs tile i's MFMAs (fragment
-  // buffer i % 2) beside tile i+1's LayerNorm (raw slot (i+1) % 3 -> buffer (i+1) % 2), so
+  // buffer i % 2) beside tile i+1's LayerNorm (raw slot (i+1) % kRing -> buffer (i+1) % 2), so
   // the LayerNorm's VALU work fills the MFMAs' issue gaps
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kDmaPerWave) : "memory");  // tile 0 landed (this wave's pieces)
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kRing - 1) * kDmaPerWave) : "memory");  // tile 0 landed (this wave's pieces)
   __builtin_amdgcn_s_barrier();
   layernorm(0);
   for (int i = 0; i < my; ++i) {
-    // tile i+1's DMA landed: after it this wave issued tile i+2's DMA (iteration i-1, or the
-    // prologue) and tiles i-2's and i-1's stores
+    // tile i+1's DMA landed: after it this wave issued the DMAs of tiles i+2 .. i+kRing-1
+    // (iterations i+2-kRing .. i-1, or the prologue) and the stores of iterations
+    // i+1-kRing .. i-1
+    static_assert(kRing == 4, "the wait counts below are those of a 4-slot ring");
     if (i == 0)
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kDmaPerWave) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * kDmaPerWave) : "memory");
     else if (i == 1)
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kDmaPerWave + kStoresPerTile) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * kDmaPerWave + kStoresPerTile) : "memory");
+    else if (i == 2)
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * kDmaPerWave + 2 * kStoresPerTile) : "memory");
     else
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kDmaPerWave + 2 * kStoresPerTile) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * kDmaPerWave + 3 * kStoresPerTile) : "memory");
     // every wave: tile i's fragments written, tile i+1's pieces landed, tile i-1's MFMAs (the
     // other fragment buffer) and tile i's LayerNorm (its raw slot) done
     __builtin_amdgcn_s_barrier();
