@@ -78,25 +78,35 @@ __global__ void __launch_bounds__(256) merge1_kernel(Merge1Params p) {
   const int my = (ntiles - (int)blockIdx.x + G - 1) / G;  // this workgroup's tiles: blockIdx.x + i G
   if (my <= 0) return;
 
+  // The raw tile [16 rows][96 16-B chunks]: chunk c of a row (gathered channels 4c .. 4c+3)
+  // sits at position 16 (c % 6) + c / 6 of the row, so the LayerNorm's 16 lanes of a row
+  // (lane l16 owns chunks 6 l16 .. 6 l16 + 5) read 16 consecutive chunks per instruction.
+  // LDS unit u = 64 piece + lane of the DMA (lane-linear) is row u / 96, position u % 96; its
+  // source offset within the tile is the same for every tile, computed here once:
+  // gathered chunk c is part c / 24 (x0 .. x3 of torchvision's cat) of pixel
+  // (2 oi + part % 2, 2 (16 jt + row) + part / 2), channels 4 (c % 24) ..
+  uint32_t doff[kDmaPerWave];
+#pragma unroll
+  for (int k = 0; k < kDmaPerWave; ++k) {
+    const int u = (wave * kDmaPerWave + k) * 64 + lane;
+    const int t = u / 96, pos = u - (u / 96) * 96;
+    const int c = 6 * (pos & 15) + (pos >> 4);
+    const int part = c / 24, ch = 4 * (c - part * 24);
+    doff[k] = (uint32_t)((((part & 1) * p.W + 2 * t + (part >> 1)) * kMC + ch) * 4);
+  }
   // the DMA of local tile i (a tile past the end re-reads the first: the ring's wait counts
   // stay those of the steady state, and the LayerNorm of "tile my" reads valid data; neither
-  // result is used)
+  // result is used); the tile's base (uniform) goes into the DMA's scalar address
   auto issue = [&](int i) __attribute__((always_inline)) {
     const int T = (int)blockIdx.x + (i < my ? i : 0) * G;
     const int b = T / (H2 * JT);
     const int rem = T - b * H2 * JT;
     const int oi = rem / JT, jt = rem - (rem / JT) * JT;
-    const char* img = reinterpret_cast<const char*>(p.X + (size_t)b * p.H * p.W * kMC);
+    const char* base = reinterpret_cast<const char*>(p.X + (((size_t)b * p.H + 2 * oi) * p.W + 2 * kMRows * jt) * kMC);
     char* dst = raw[i % kRing];
 #pragma unroll
-    for (int k = 0; k < kDmaPerWave; ++k) {
-      const int piece = wave * kDmaPerWave + k;
-      const int u = piece * 64 + lane;  // 16-B unit of the tile's [16][384] fp32 image
-      const int t = u / 96, q = u - (u / 96) * 96;
-      const int part = q / 24, c = 4 * (q - part * 24);
-      const int py = 2 * oi + (part & 1), px = 2 * (jt * kMRows + t) + (part >> 1);
-      dma16(img, (uint32_t)(((size_t)py * p.W + px) * kMC + c) * 4u, lds_u32(dst + piece * 1024));
-    }
+    for (int k = 0; k < kDmaPerWave; ++k)
+      dma16(base, doff[k], lds_u32(dst + (wave * kDmaPerWave + k) * 1024));
   };
 #pragma unroll
   for (int i = 0; i < kRing; ++i) issue(i);
@@ -120,11 +130,11 @@ __global__ void __launch_bounds__(256) merge1_kernel(Merge1Params p) {
   const int j16 = lane & 15, g = lane >> 4;
   // LayerNorm of tile i's row `row`, channels 24 l16 .. + 23, into B-fragment buffer i % 2
   auto layernorm = [&](int i) __attribute__((always_inline)) {
-    const float* xr = reinterpret_cast<const float*>(raw[i % kRing]) + row * kMK + 24 * l16;
+    const float* xr = reinterpret_cast<const float*>(raw[i % kRing]) + row * kMK + 4 * l16;
     float v[24];
 #pragma unroll
     for (int e = 0; e < 6; ++e) {
-      const floatx4 a = *reinterpret_cast<const floatx4*>(xr + 4 * e);
+      const floatx4 a = *reinterpret_cast<const floatx4*>(xr + 64 * e);  // chunk 6 l16 + e
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[4 * e + r] = a[r];
     }
@@ -150,7 +160,9 @@ __global__ void __launch_bounds__(256) merge1_kernel(Merge1Params p) {
       }
       bf16x8 hi, lo;
       split8(y, hi, lo);
-      const int fl = (k8 & 3) * 16 + row;  // fragment lane: lane group, row
+      // fragment lane (lane group k8 % 4, row) at slot row ^ (k8 % 16) of its lane group: the
+      // 16 lanes of a row write 16 distinct slots (k8 = 3 l16 + h is distinct mod 16)
+      const int fl = (k8 & 3) * 16 + (row ^ (k8 & 15));
       char* fp = frag[i & 1] + ((k8 >> 2) * 2 * 64 + fl) * 16;
       *reinterpret_cast<bf16x8*>(fp) = hi;
       if constexpr (X3) *reinterpret_cast<bf16x8*>(fp + 1024) = lo;
@@ -187,7 +199,7 @@ __global__ void __launch_bounds__(256) merge1_kernel(Merge1Params p) {
     const char* fb = frag[i & 1];
 #pragma unroll
     for (int ks = 0; ks < 12; ++ks) {
-      const char* fp = fb + (ks * 2 * 64 + lane) * 16;
+      const char* fp = fb + (ks * 2 * 64 + 16 * g + (j16 ^ ((4 * ks + g) & 15))) * 16;
       const bf16x8 bh = *reinterpret_cast<const bf16x8*>(fp);
       bf16x8 bl;
       if constexpr (X3) bl = *reinterpret_cast<const bf16x8*>(fp + 1024);
