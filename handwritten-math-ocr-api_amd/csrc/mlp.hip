@@ -656,27 +656,28 @@ __global__ void __launch_bounds__(64 * NW) mlp384_kernel(MlpParams p) {
     for (int i = tid; i < C; i += 64 * NW) bps[i] = p.bproj[perm384(i)];
 
   // GEMM 2's loop body over one W2-geometry chunk in slot `ws`: out^T [384 x 32] +=
-  // W[:, chunk] . B^T, one channel tile per step, the next tile's fragments read ahead,
+  // W[:, chunk] . B^T, one channel tile per step, the fragments read two tiles ahead,
   // one DMA piece of the item two ahead issued every other step
   auto gemm2 = [&](const char* ws, auto bf, const char* nbase, int njc, char* ndst, bool nxt)
                    __attribute__((always_inline)) {
-    bf16x8 fb[2][PL];
+    bf16x8 fb[3][PL];
     auto rd2 = [&](int ct, bf16x8(&f)[PL]) {
       const int o = fo + ct * 1024;
       f[0] = *reinterpret_cast<const bf16x8*>(ws + o);
       if constexpr (X3) f[PL - 1] = *reinterpret_cast<const bf16x8*>(ws + PLB + o);
     };
     rd2(0, fb[0]);
+    rd2(1, fb[1]);
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct) {
-      if (ct + 1 < NCT) rd2(ct + 1, fb[(ct + 1) & 1]);
+      if (ct + 2 < NCT) rd2(ct + 2, fb[(ct + 2) % 3]);
       if (nxt && (ct & 1) == 0 && ct / 2 < NPW) issue(nbase, njc, ndst, ct / 2, 1);
 #pragma unroll
       for (int tt = 0; tt < TT; ++tt) {
-        const bf16x8 ah = fb[ct & 1][0];
+        const bf16x8 ah = fb[ct % 3][0];
         acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bf(tt, 0), acc2[ct][tt], 0, 0, 0);
         if constexpr (X3) {
-          const bf16x8 al = fb[ct & 1][PL - 1];
+          const bf16x8 al = fb[ct % 3][PL - 1];
           acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bf(tt, 1), acc2[ct][tt], 0, 0, 0);
           acc2[ct][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bf(tt, 0), acc2[ct][tt], 0, 0, 0);
         }
