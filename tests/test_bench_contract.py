@@ -72,10 +72,12 @@ def test_e2e_roofline_is_baseline_md_section4(bench):
 def test_committed_pmc_traffic_covers_the_roofline_classes(bench):
     # the bench's roofline classes at its default 8 x 64 and the driver's 10 x 64 images per
     # call (round 3's 4 x 64 profile kept, from before stage 3's fused attention ran at
-    # every batch: its norm1 + qkv was s3.lnqkv)
+    # every batch: its norm1 + qkv was s3.lnqkv; round 6's profiles have the block tail
+    # s3.tail where the proj GEMM and s3.mlp were, and merge 1 as one kernel)
     for batch in (256, 512, 640):
         s3 = "s3.lnqkv" if batch == 256 else "s3.attn"
-        for cls in ("s3.mlp", "s1.attn", s3, "decode.step"):
+        tail = "s3.mlp" if batch == 256 else "s3.tail"
+        for cls in (tail, "s1.attn", s3, "decode.step") + (("merge1",) if batch != 256 else ()):
             t = bench.pmc_traffic("bf16x3", cls, batch)
             assert t is not None and t > 0, (batch, cls)
     assert bench.pmc_traffic("bf16x3", "no.such.class", 512) is None
