@@ -94,15 +94,42 @@ __global__ void __launch_bounds__(256) merge1_kernel(Merge1Params p) {
     const int part = c / 24, ch = 4 * (c - part * 24);
     doff[k] = (uint32_t)((((part & 1) * p.W + 2 * t + (part >> 1)) * kMC + ch) * 4);
   }
-  // the DMA of local tile i (a tile past the end re-reads the first: the ring's wait counts
-  // stay those of the steady state, and the LayerNorm of "tile my" reads valid data; neither
-  // result is used); the tile's base (uniform) goes into the DMA's scalar address
+  // Tile T = (image b, output row oi, 16-pixel column block jt); local tile i is blockIdx.x +
+  // i G.  Two cursors walk this workgroup's tiles, one for the DMA (kRing tiles ahead) and
+  // one for the stores, advanced by G's own decomposition with carries (scalar adds instead
+  // of three integer divisions per tile and cursor)
+  const int HJ = H2 * JT;
+  const int gb = G / HJ, grem = G - (G / HJ) * HJ, goi = grem / JT, gjt = grem - (grem / JT) * JT;
+  struct Cur {
+    int b, oi, jt;
+  };
+  const int r0 = (int)blockIdx.x - ((int)blockIdx.x / HJ) * HJ;
+  const Cur first = {(int)blockIdx.x / HJ, r0 / JT, r0 - (r0 / JT) * JT};
+  auto step = [&](Cur& c) __attribute__((always_inline)) {
+    c.jt += gjt;
+    c.oi += goi;
+    c.b += gb;
+    if (c.jt >= JT) {
+      c.jt -= JT;
+      ++c.oi;
+    }
+    if (c.oi >= H2) {
+      c.oi -= H2;
+      ++c.b;
+    }
+  };
+  auto in_base = [&](const Cur& c) __attribute__((always_inline)) {
+    return reinterpret_cast<const char*>(p.X + (((size_t)c.b * p.H + 2 * c.oi) * p.W + 2 * kMRows * c.jt) * kMC);
+  };
+  const char* const base0 = in_base(first);
+  Cur dcur = first;
+  // the DMA of local tile i, issued in order (a tile past the end re-reads the first: the
+  // ring's wait counts stay those of the steady state, and the LayerNorm of "tile my" reads
+  // valid data; neither result is used); the tile's base (uniform) goes into the DMA's
+  // scalar address
   auto issue = [&](int i) __attribute__((always_inline)) {
-    const int T = (int)blockIdx.x + (i < my ? i : 0) * G;
-    const int b = T / (H2 * JT);
-    const int rem = T - b * H2 * JT;
-    const int oi = rem / JT, jt = rem - (rem / JT) * JT;
-    const char* base = reinterpret_cast<const char*>(p.X + (((size_t)b * p.H + 2 * oi) * p.W + 2 * kMRows * jt) * kMC);
+    const char* base = i < my ? in_base(dcur) : base0;
+    step(dcur);
     char* dst = raw[i % kRing];
 #pragma unroll
     for (int k = 0; k < kDmaPerWave; ++k)
@@ -175,6 +202,7 @@ __global__ void __launch_bounds__(256) merge1_kernel(Merge1Params p) {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kRing - 1) * kDmaPerWave) : "memory");  // tile 0 landed (this wave's pieces)
   __builtin_amdgcn_s_barrier();
   layernorm(0);
+  Cur scur = first;  // the store cursor: tile i
   for (int i = 0; i < my; ++i) {
     // tile i+1's DMA landed: after it this wave issued the DMAs of tiles i+2 .. i+kRing-1
     // (iterations i+2-kRing .. i-1, or the prologue) and the stores of iterations
@@ -215,11 +243,8 @@ __global__ void __launch_bounds__(256) merge1_kernel(Merge1Params p) {
     layernorm(i + 1);  // independent of the MFMAs above: the scheduler interleaves them
     // lane (g, j16): output row j16, channels 16 (3 wave + t) + 4 g .. + 3
     {
-      const int T = (int)blockIdx.x + i * G;
-      const int b = T / (H2 * JT);
-      const int rem = T - b * H2 * JT;
-      const int oi = rem / JT, jt = rem - (rem / JT) * JT;
-      float* o = p.out + (((size_t)b * H2 + oi) * W2 + jt * kMRows + j16) * kMN + 48 * wave + 4 * g;
+      float* o = p.out + (((size_t)scur.b * H2 + scur.oi) * W2 + scur.jt * kMRows + j16) * kMN + 48 * wave + 4 * g;
+      step(scur);
 #pragma unroll
       for (int t = 0; t < 3; ++t) *reinterpret_cast<floatx4*>(o + 16 * t) = acc[t];
     }
